@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the hot path: Compressor2018 forward + RD loss +
+backward (+ RCCL gradient all-reduce when N > 1) on synthetic 256x256 batches.
+
+Workload (BASELINE.json configs[1], "C2"): psnr_256 semantics — lambda=256,
+MSE distortion, Laplacian conditional, 192/192 channels, fp32, batch 32 per
+GPU (weak scaling: the per-GPU batch stays 32 as N grows).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `roofline` times the dominant kernel (the
+implicit-GEMM conv, measured on the analysis transform's 128->64 5x5 192->192
+layer) with events on the launch stream; `cpu_baseline` times the CPU oracle
+(oracle/ref_cpu.py, a restatement of the reference path) on a bounded sample
+on this host.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+FP32_PEAK_TFLOPS = 157.3          # MI355X dense fp32 (matrix = vector), MI355X_MICROARCH.md
+FWD_GMAC_PER_IMG = 12.2837        # SURVEY.md 6.2 (latent 192, 256x256)
+STEP_GFLOP_PER_IMG = 3 * 2 * FWD_GMAC_PER_IMG   # fwd + dgrad + wgrad = 73.70
+METRIC = "256x256 images/s fwd+bwd at 1/2/4/8 GPUs; bpp & PSNR vs ref on Kodak"
+
+
+def _cfg(lam=256.0):
+    from image_compression_amd import get_cfg_defaults
+    cfg = get_cfg_defaults()
+    cfg.MODEL.LOSS.REDUCTION = "mean"
+    cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT = lam
+    return cfg
+
+
+def dominant_kernel_roofline(dev, reps=20):
+    """Average duration of the implicit-GEMM conv kernel on g_a layer 2
+    (conv 5x5 s2, 192->192, 128x128 -> 64x64, batch 32): one launch =
+    2 * (32*64*64) * 192 * (25*192) = 241.6 GFLOP of algorithmic work."""
+    from image_compression_amd import functional as IF
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand(32, 192, 128, 128, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(192, 192, 5, 5, device=dev, generator=g) * 0.02
+    b = torch.zeros(192, device=dev)
+    flop = 2.0 * (32 * 64 * 64) * 192 * (25 * 192)
+    with torch.no_grad():
+        for _ in range(3):
+            IF.conv2d(x, w, b, 2, 2)
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            IF.conv2d(x, w, b, 2, 2)
+        e1.record(st)
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    achieved = flop / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "ig_kernel<128,192,64,96> + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
+            "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}
+
+
+def cpu_baseline(seconds_target=12.0):
+    """The CPU oracle (torch CPU restatement of the reference path) on a
+    bounded sample: batch 8, 256x256, fwd + RD loss + bwd."""
+    from image_compression_amd import modelling
+    from oracle import ref_cpu
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    params = {k: v.clone() for k, v in modelling.build_model(_cfg()).state_dict().items()}
+    g = torch.Generator().manual_seed(0)
+    N = 8
+    x = torch.rand(N, 3, 256, 256, generator=g)
+    uz = torch.rand(N, 192, 4, 4, generator=g)
+    uy = torch.rand(N, 192, 16, 16, generator=g)
+    ref_cpu.run(params, x, uz, uy, train=True, dtype=torch.float32, lam=256.0)  # warm-up
+    t0 = time.perf_counter()
+    iters = 0
+    while True:
+        ref_cpu.run(params, x, uz, uy, train=True, dtype=torch.float32, lam=256.0)
+        iters += 1
+        if time.perf_counter() - t0 >= seconds_target or iters >= 10:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(N * iters / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} iteration(s) of batch {N} at 256x256 fp32 fwd+loss+bwd "
+                      f"(oracle/ref_cpu.py, torch CPU, {threads} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--profile-step-only", action="store_true",
+                    help="only warmup+timed steps (for rocprofv3 runs)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from image_compression_amd import modelling
+    torch.manual_seed(0)
+    model = modelling.build_model(_cfg()).to(dev).train()
+    if dist:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        model = DDP(model, device_ids=[local], bucket_cap_mb=12, gradient_as_bucket_view=True,
+                    broadcast_buffers=False)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        _, losses = model(x)
+        losses["total_loss"].backward()
+        return losses
+
+    for _ in range(args.warmup):
+        losses = step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    bpp = float(losses["bpp"])
+    mse = float(losses["MSE"])
+    if args.profile_step_only:
+        if rank == 0:
+            print(json.dumps({"ms_per_step": 1e3 * elapsed / args.steps}))
+        if dist:
+            tdist.destroy_process_group()
+        return
+
+    images = args.batch * world * args.steps
+    value = images / elapsed
+    ms = 1e3 * elapsed / args.steps
+    roof = None if args.no_roofline else dominant_kernel_roofline(dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    if rank == 0:
+        step_tflops = value / world * STEP_GFLOP_PER_IMG * (args.size / 256) ** 2 / 1e3
+        rec = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic: torch.rand uniform [0,1) images resident in HBM; random-init weights "
+                    "(reference init, seed 0); training noise from in-kernel Philox",
+            "config": {"workload": "C2: psnr_256 (lambda=256, MSE, Laplacian conditional, 192/192 ch), "
+                                   f"{args.size}x{args.size}, {args.batch} images/GPU, fwd+loss+bwd"
+                                   + (" + RCCL grad all-reduce (DDP, 12 MB buckets)" if dist else ""),
+                       "global_batch": args.batch * world, "image_size": args.size,
+                       "parallelism": f"dp{world}"},
+            "model_tflops_per_gpu": round(step_tflops, 2),
+            "model_mfma_frac": round(step_tflops / FP32_PEAK_TFLOPS, 4),
+            "bpp": round(bpp, 4), "mse": mse,
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec))
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+"""ctypes binding of libimgcomp.so (the C ABI declared in include/imgcomp.h).
+
+The shared library is built in-tree by `make -C image_compression_amd/csrc`
+(or `__graft_entry__.build()`).  There is no fallback: if the library or a
+ROCm device is missing, every op raises RuntimeError.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported first: shares its HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libimgcomp.so")
+
+c_int, c_ll, c_ull, c_size, c_float, c_void = (ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                              ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p)
+
+
+class ICAct(ctypes.Structure):
+    _fields_ = [("data", c_void), ("n", c_int), ("c", c_int), ("h", c_int), ("w", c_int),
+                ("sn", c_ll), ("sc", c_ll), ("sh", c_ll), ("sw", c_ll)]
+
+
+_FACT_FIELDS = ["w0", "b0", "f0", "w1", "b1", "f1", "w2", "b2", "f2", "w3", "b3"]
+
+
+class ICFactParams(ctypes.Structure):
+    _fields_ = [(f, c_void) for f in _FACT_FIELDS]
+
+
+class ICFactGrads(ctypes.Structure):
+    _fields_ = [(f, c_void) for f in _FACT_FIELDS]
+
+
+P = ctypes.POINTER
+_ACT = P(ICAct)
+
+# name -> (restype, argtypes); mirrors include/imgcomp.h one to one
+SIGNATURES = {
+    "ic_version": (c_int, []),
+    "ic_device_sync_check": (c_int, [c_void]),
+    "ic_conv2d_fwd_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),
+    "ic_conv2d_fwd": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size, c_void]),
+    "ic_conv2d_dgrad_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),
+    "ic_conv2d_dgrad": (c_int, [_ACT, c_void, c_int, c_int, c_int, _ACT, c_void, c_size, c_void]),
+    "ic_conv2d_wgrad_ws": (c_size, [_ACT, _ACT, c_int, c_int, c_int]),
+    "ic_conv2d_wgrad": (c_int, [_ACT, _ACT, c_int, c_int, c_int, c_void, c_void, c_void, c_size, c_void]),
+    "ic_conv_transpose2d_fwd_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),
+    "ic_conv_transpose2d_fwd": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size, c_void]),
+    "ic_conv_transpose2d_dgrad_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),
+    "ic_conv_transpose2d_dgrad": (c_int, [_ACT, c_void, c_int, c_int, c_int, _ACT, c_void, c_size, c_void]),
+    "ic_conv_transpose2d_wgrad_ws": (c_size, [_ACT, _ACT, c_int, c_int, c_int]),
+    "ic_conv_transpose2d_wgrad": (c_int, [_ACT, _ACT, c_int, c_int, c_int, c_void, c_void, c_void, c_size, c_void]),
+    "ic_gdn_fwd_ws": (c_size, [_ACT]),
+    "ic_gdn_fwd": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_void, c_size, c_void]),
+    "ic_gdn_bwd_ws": (c_size, [_ACT]),
+    "ic_gdn_bwd": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_size, c_void]),
+    "ic_nonneg_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void]),
+    "ic_nonneg_bwd": (c_int, [c_void, c_void, c_ll, c_float, c_void, c_void]),
+    "ic_bound_fwd": (c_int, [c_void, c_ll, c_float, c_int, c_void, c_void]),
+    "ic_bound_bwd": (c_int, [c_void, c_void, c_ll, c_float, c_int, c_void, c_void]),
+    "ic_relu_fwd": (c_int, [c_void, c_ll, c_void, c_void]),
+    "ic_relu_bwd": (c_int, [c_void, c_void, c_ll, c_void, c_void]),
+    "ic_abs_fwd": (c_int, [c_void, c_ll, c_void, c_void]),
+    "ic_abs_bwd": (c_int, [c_void, c_void, c_ll, c_void, c_void]),
+    "ic_exp_clamp_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void, c_void]),
+    "ic_exp_clamp_bwd": (c_int, [c_void, c_void, c_ll, c_float, c_float, c_void, c_void]),
+    "ic_reduce_ws": (c_size, [c_ll]),
+    "ic_ce_loss_fwd": (c_int, [c_void, c_ll, c_void, c_void, c_size, c_void]),
+    "ic_ce_loss_bwd": (c_int, [c_void, c_void, c_ll, c_void, c_void]),
+    "ic_mse_fwd": (c_int, [c_void, c_void, c_ll, c_void, c_void, c_size, c_void]),
+    "ic_mse_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
+    "ic_uniform": (c_int, [c_void, c_ll, c_ull, c_ull, c_void]),
+    "ic_factorized_fwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),
+    "ic_factorized_bwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_void, c_void, c_void, P(ICFactGrads), c_void]),
+    "ic_conditional_fwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),
+    "ic_conditional_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_void, c_void, c_void, c_void, c_void, c_void]),
+    "ic_msssim_state_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "ic_msssim_ws": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "ic_msssim_fwd": (c_int, [c_void, c_void, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int,
+                              c_int, c_float, c_float, c_float, c_void, c_void, c_void, c_void, c_size, c_void]),
+    "ic_msssim_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_float,
+                              c_float, c_float, c_void, c_void, c_void, c_void, c_void, c_void, c_size, c_void]),
+    "ic_sqdiff_fwd": (c_int, [c_void, c_void, c_ll, c_void, c_void]),
+    "ic_sqdiff_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load libimgcomp.so once; raise RuntimeError (never fall back) on failure."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"imgcomp: HIP library not built ({LIB_PATH} missing); run "
+            "`make -C image_compression_amd/csrc` or __graft_entry__.build()")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise RuntimeError(f"imgcomp: cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        if not hasattr(lib, name):
+            continue  # reported by exported_symbols()/tests
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    lib = load()
+    return {n for n in SIGNATURES if hasattr(lib, n)}
+
+
+def check(rc, what):
+    if rc != 0:
+        kind = {1001: "unsupported/inconsistent arguments", 1002: "workspace too small"}.get(rc, "HIP error")
+        raise RuntimeError(f"imgcomp: {what} failed with status {rc} ({kind})")
+
+
+def act(t):
+    """ic_act for a 4-D tensor (logical N,C,H,W, any strides)."""
+    if t.dim() != 4:
+        raise RuntimeError(f"imgcomp: expected a 4-D tensor, got shape {tuple(t.shape)}")
+    s = t.stride()
+    return ICAct(c_void(t.data_ptr()), t.shape[0], t.shape[1], t.shape[2], t.shape[3], s[0], s[1], s[2], s[3])
+
+
+def ptr(t):
+    return None if t is None else c_void(t.data_ptr())
+
+
+def stream_of(t):
+    return c_void(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("imgcomp: HIP kernels need tensors on a ROCm (cuda) device; "
+                               f"got a tensor on {t.device}")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"imgcomp: fp32 tensors expected, got {t.dtype}")
+
+
+def workspace(nbytes, device):
+    n = max(int(nbytes), 16)
+    return torch.empty(n, dtype=torch.uint8, device=device)

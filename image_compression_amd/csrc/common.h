@@ -1,0 +1,94 @@
+// Shared device/host helpers for the gfx950 (CDNA4) kernels of imgcomp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+
+#define IC_MAXT 25      // max taps of one (phase of a) convolution: 5x5
+#define IC_MAXPH 4      // max sub-pixel phases per launch (stride 2)
+
+// status codes returned by every extern "C" entry point (0 = ok)
+#define IC_OK 0
+#ifndef IC_ERR_ARG
+#define IC_ERR_ARG 1001        // unsupported / inconsistent arguments
+#define IC_ERR_WORKSPACE 1002  // workspace too small
+#endif
+
+#define IC_CHECK_LAUNCH()                                    \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return (int)_e;                    \
+  } while (0)
+
+static inline size_t ic_align(size_t v, size_t a) { return (v + a - 1) / a * a; }
+static inline int ic_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Fast unsigned division for numerators < 2^31 (Granlund-Montgomery):
+// q = (umulhi(n, m) + n) >> l, with l = ceil(log2 d), m = 2^32 (2^l - d) / d + 1.
+struct FastDiv {
+  uint32_t d, m, l;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d ? d : 1;
+  f.l = 0;
+  while ((1ull << f.l) < f.d) ++f.l;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << f.l) - f.d)) / f.d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.l;
+}
+
+// 64-lane wave reduction (gfx950 wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block reduction of `nv` values per thread (blockDim.x multiple of 64,
+// <= 1024).  Result valid in thread 0.  Deterministic order.
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* lds /* >= 16*NV */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) lds[wid * NV + i] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float s = 0.f;
+      for (int w = 0; w < nw; ++w) s += lds[w * NV + i];
+      v[i] = s;
+    }
+  }
+  __syncthreads();
+}
+
+// Philox4x32-10 counter-based RNG -> uniform float in [0,1) (24-bit mantissa)
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+  uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+  uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
+  c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+}
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx) {
+  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), 0x9E3779B9u, 0x3C6EF372u};
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k0, k1);
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}

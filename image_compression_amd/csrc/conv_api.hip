@@ -1,0 +1,248 @@
+// C-ABI convolution entry points (conv2d / conv_transpose2d: fwd, dgrad, wgrad)
+// built on the two gather-GEMM kernel families of igemm.hip / wgrad.hip.
+//
+//   conv fwd       = "direct"     gather (stride s, taps dy = ky - pad)
+//   conv dgrad     = "transposed" gather (s*s sub-pixel phases)
+//   tconv fwd      = "transposed" gather (+bias, +act)
+//   tconv dgrad    = "direct"     gather
+//   conv wgrad     = wgrad(G = dy, X = x)
+//   tconv wgrad    = wgrad(G = x,  X = dy)   (same index relation)
+#include "../../include/imgcomp.h"
+#include "gemm.h"
+
+namespace {
+
+struct Carve {
+  char* base;
+  size_t off;
+  float* take(size_t bytes) {
+    float* p = (float*)(base + off);
+    off += ic_align(bytes, 256);
+    return p;
+  }
+};
+
+void set_x(IgDesc& d, const ic_act* x) {
+  d.x = x->data; d.xs_n = x->sn; d.xs_h = x->sh; d.xs_w = x->sw; d.xs_c = x->sc;
+  d.Hx = x->h; d.Wx = x->w; d.Cin = x->c; d.N = x->n;
+}
+void set_y(IgDesc& d, const ic_act* y) {
+  d.y = y->data; d.ys_n = y->sn; d.ys_h = y->sh; d.ys_w = y->sw; d.ys_c = y->sc; d.Cout = y->c;
+}
+
+// y[a] = sum_{t,b} x[b] @ (gy*s + ky - pad) * W[a][b][ky][kx]   (W: [A=y->c][B=x->c][k][k])
+int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
+                const ic_act* y, int epi, int aop, const float* aux0, const float* aux1,
+                const float* aux2, float* aux_out, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
+  if (x->n != y->n) return IC_ERR_ARG;
+  if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w)
+    return IC_ERR_ARG;
+  IgDesc d = {};
+  set_x(d, x);
+  set_y(d, y);
+  d.stride = stride;
+  d.generic = (x->c % 32 != 0) || (x->sc != 1);
+  d.bias = bias; d.epi = epi; d.a_op = aop;
+  d.aux0 = aux0; d.aux1 = aux1; d.aux2 = aux2; d.aux_out = aux_out;
+  d.nphase = 1;
+  IgPhase& P = d.ph[0];
+  P.T = k * k;
+  int ky[IC_MAXT], kx[IC_MAXT];
+  for (int t = 0; t < P.T; ++t) {
+    ky[t] = t / k; kx[t] = t % k;
+    P.dy[t] = ky[t] - pad; P.dx[t] = kx[t] - pad;
+  }
+  P.Hg = y->h; P.Wg = y->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;
+  d.Kc = d.generic ? (int)ic_align((size_t)P.T * x->c, 32) : x->c;
+  const size_t part = ig_plan(d);
+  const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * 4;
+  const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
+  if (need) { *need = tot; return IC_OK; }
+  if (wsb < tot) return IC_ERR_WORKSPACE;
+  Carve cv{(char*)ws, 0};
+  float* wp = cv.take(wpb);
+  d.partial = part ? cv.take(part) : nullptr;
+  P.wp = wp;
+  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s);
+  if (rc) return rc;
+  return ig_run(d, s);
+}
+
+// y[b] at (s*iy - pad + ky) += x[a] @ iy * W[a][b][ky][kx]    (W: [A=x->c][B=y->c][k][k])
+int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
+                    const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  if (k < 1 || k * k > IC_MAXT || stride < 1 || stride > 2) return IC_ERR_ARG;
+  if (x->n != y->n) return IC_ERR_ARG;
+  if ((y->h + 2 * pad - k) / stride + 1 != x->h || (y->w + 2 * pad - k) / stride + 1 != x->w)
+    return IC_ERR_ARG;
+  IgDesc d = {};
+  set_x(d, x);
+  set_y(d, y);
+  d.stride = 1;
+  d.generic = (x->c % 32 != 0) || (x->sc != 1);
+  d.bias = bias; d.epi = epi; d.a_op = AOP_NONE;
+  int pky[IC_MAXPH][IC_MAXT], pkx[IC_MAXPH][IC_MAXT];
+  int np = 0, tmax = 0;
+  for (int py = 0; py < stride; ++py)
+    for (int px = 0; px < stride; ++px) {
+      IgPhase& P = d.ph[np];
+      const int Hg = (y->h - py + stride - 1) / stride, Wg = (y->w - px + stride - 1) / stride;
+      if (Hg <= 0 || Wg <= 0) continue;
+      int T = 0;
+      for (int a = 0; a < k; ++a) {
+        const int ny = py + pad - a;
+        if (((ny % stride) + stride) % stride) continue;
+        for (int b = 0; b < k; ++b) {
+          const int nx = px + pad - b;
+          if (((nx % stride) + stride) % stride) continue;
+          pky[np][T] = a; pkx[np][T] = b;
+          P.dy[T] = ny / stride;  // exact division (ny multiple of stride)
+          P.dx[T] = nx / stride;
+          ++T;
+        }
+      }
+      if (T == 0) return IC_ERR_ARG;
+      P.T = T; P.Hg = Hg; P.Wg = Wg;
+      P.oys = stride; P.oxs = stride; P.oy0 = py; P.ox0 = px;
+      tmax = T > tmax ? T : tmax;
+      ++np;
+    }
+  d.nphase = np;
+  d.Kc = d.generic ? (int)ic_align((size_t)tmax * x->c, 32) : x->c;
+  const size_t part = ig_plan(d);
+  size_t wpb[IC_MAXPH];
+  size_t tot = ic_align(part, 256);
+  for (int p = 0; p < np; ++p) {
+    wpb[p] = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)d.ph[p].T * d.Npad * x->c * 4;
+    tot += ic_align(wpb[p], 256);
+  }
+  if (need) { *need = tot; return IC_OK; }
+  if (wsb < tot) return IC_ERR_WORKSPACE;
+  Carve cv{(char*)ws, 0};
+  d.partial = part ? cv.take(part) : nullptr;
+  for (int p = 0; p < np; ++p) {
+    float* wp = cv.take(wpb[p]);
+    d.ph[p].wp = wp;
+    int rc = pack_weights(W, x->c, y->c, k, 1, d.generic, d.ph[p].T, pky[p], pkx[p], d.Npad, d.Kc, wp, s);
+    if (rc) return rc;
+  }
+  return ig_run(d, s);
+}
+
+// dW[g][c][ky][kx] = sum_p G[p][g] * X[p*s + ky - pad][c]; db = colsum(bias_src)
+int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, float* dw,
+               const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
+  if (G->n != X->n) return IC_ERR_ARG;
+  if ((X->h + 2 * pad - k) / stride + 1 != G->h || (X->w + 2 * pad - k) / stride + 1 != G->w)
+    return IC_ERR_ARG;
+  WgDesc d = {};
+  d.g = G->data; d.gs_n = G->sn; d.gs_h = G->sh; d.gs_w = G->sw; d.gs_c = G->sc;
+  d.Hg = G->h; d.Wg = G->w; d.Cg = G->c;
+  d.x = X->data; d.xs_n = X->sn; d.xs_h = X->sh; d.xs_w = X->sw; d.xs_c = X->sc;
+  d.Hx = X->h; d.Wx = X->w; d.Cx = X->c;
+  d.N = G->n; d.stride = stride; d.T = k * k; d.x_op = AOP_NONE;
+  d.generic = (X->c % 4 != 0) || (X->sc != 1);
+  int kk_of_t[IC_MAXT];
+  for (int t = 0; t < d.T; ++t) {
+    d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
+  }
+  const size_t part = wg_plan(d);
+  const size_t cs = db ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
+  const size_t tot = ic_align(part, 256) + ic_align(cs, 256);
+  if (need) { *need = tot; return IC_OK; }
+  if (wsb < tot) return IC_ERR_WORKSPACE;
+  Carve cv{(char*)ws, 0};
+  d.partial = cv.take(part);
+  float* csw = cs ? cv.take(cs) : nullptr;
+  int rc = wg_run(d, s);
+  if (rc) return rc;
+  rc = wg_reduce(d, dw, kk_of_t, k * k, s);
+  if (rc) return rc;
+  if (db) {
+    rc = colsum(bias_src->data, bias_src->sn, bias_src->sc, bias_src->sh, bias_src->sw, bias_src->n,
+                bias_src->c, bias_src->h, bias_src->w, db, 1.f, csw, s);
+    if (rc) return rc;
+  }
+  return IC_OK;
+}
+
+size_t need_or_zero(int rc, size_t n) { return rc ? 0 : n; }
+
+}  // namespace
+
+extern "C" {
+
+int ic_version(void) { return 1; }
+
+size_t ic_conv2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+  size_t n = 0;
+  int rc = direct_impl(x, nullptr, nullptr, k, stride, pad, y, EPI_NONE, AOP_NONE, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                  const ic_act* y, int act, void* ws, size_t ws_bytes, void* stream) {
+  return direct_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, AOP_NONE, nullptr,
+                     nullptr, nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+  size_t n = 0;
+  int rc = transposed_impl(dy, nullptr, nullptr, k, stride, pad, dx, EPI_NONE, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx,
+                    void* ws, size_t ws_bytes, void* stream) {
+  // conv weight [Cout][Cin] is the transposed-gather weight [A=Cout (dy ch)][B=Cin (dx ch)]
+  return transposed_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, ws, ws_bytes,
+                         (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {
+  size_t n = 0;
+  int rc = wgrad_impl(dy, x, k, stride, pad, nullptr, dy, (float*)1, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw,
+                    float* db, void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(dy, x, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv_transpose2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+  size_t n = 0;
+  int rc = transposed_impl(x, nullptr, nullptr, k, stride, pad, y, EPI_NONE, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride,
+                            int pad, const ic_act* y, int act, void* ws, size_t ws_bytes,
+                            void* stream) {
+  return transposed_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, ws, ws_bytes,
+                         (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv_transpose2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+  size_t n = 0;
+  int rc = direct_impl(dy, nullptr, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad,
+                              const ic_act* dx, void* ws, size_t ws_bytes, void* stream) {
+  // tconv weight [Cin][Cout] is the direct-gather weight [A=Cin (dx ch)][B=Cout (dy ch)]
+  return direct_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
+                     nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {
+  size_t n = 0;
+  int rc = wgrad_impl(x, dy, k, stride, pad, nullptr, dy, (float*)1, nullptr, 0, 0, &n);
+  return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad,
+                              float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(x, dy, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+}  // extern "C"

@@ -1,0 +1,267 @@
+// Elementwise ops and deterministic reductions of the hot path (HBM-bound).
+// All operate on dense storage of n fp32 elements; float4 vectorised where the
+// pointer alignment allows (Guideline 13), grid-stride otherwise.
+#include "../../include/imgcomp.h"
+#include "common.h"
+
+namespace {
+
+constexpr float LN2F = 0.693147180559945309f;
+
+inline unsigned grid_for(long long n, int per_thread = 1) {
+  long long b = (n / per_thread + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+__global__ void nonneg_fwd_k(const float* p, long long n, float bound, float ped, float* out) {
+  GRID_STRIDE(i, n) {
+    const float v = fmaxf(p[i], bound);
+    out[i] = v * v - ped;
+  }
+}
+// LowerBound backward (bound.py:36-42) on g_v = 2 v g_out
+__global__ void nonneg_bwd_k(const float* p, const float* go, long long n, float bound, float* gi) {
+  GRID_STRIDE(i, n) {
+    const float x = p[i];
+    const float v = fmaxf(x, bound);
+    const float g = go[i] * v * 2.f;  // d(v*v)/dv = 2v (autograd: g*v + g*v)
+    gi[i] = (x >= bound || g < 0.f) ? g : 0.f;
+  }
+}
+
+__global__ void bound_fwd_k(const float* x, long long n, float b, int upper, float* y) {
+  GRID_STRIDE(i, n) {
+    const float v = x[i];
+    y[i] = upper ? (v < b ? v : b) : (v > b ? v : b);
+  }
+}
+__global__ void bound_bwd_k(const float* x, const float* g, long long n, float b, int upper, float* gx) {
+  GRID_STRIDE(i, n) {
+    const float v = x[i], gg = g[i];
+    const bool pass = upper ? (v <= b || gg > 0.f) : (v >= b || gg < 0.f);
+    gx[i] = pass ? gg : 0.f;
+  }
+}
+
+__global__ void relu_fwd_k(const float* x, long long n, float* y) {
+  GRID_STRIDE(i, n) {
+    const float v = x[i];
+    y[i] = v > 0.f ? v : (v != v ? v : 0.f);
+  }
+}
+// torch threshold_backward: grad where result > 0
+__global__ void relu_bwd_k(const float* y, const float* g, long long n, float* gx) {
+  GRID_STRIDE(i, n) gx[i] = y[i] > 0.f ? g[i] : 0.f;
+}
+__global__ void abs_fwd_k(const float* x, long long n, float* y) {
+  GRID_STRIDE(i, n) y[i] = fabsf(x[i]);
+}
+// d|x|/dx = sign(x) (0 at 0)
+__global__ void abs_bwd_k(const float* x, const float* g, long long n, float* gx) {
+  GRID_STRIDE(i, n) {
+    const float v = x[i];
+    const float sg = v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
+    gx[i] = g[i] * sg;
+  }
+}
+__global__ void exp_clamp_fwd_k(const float* v, long long n, float lo, float hi, float* s, float* e) {
+  GRID_STRIDE(i, n) {
+    const float ev = expf(v[i]);
+    if (e) e[i] = ev;
+    s[i] = fminf(fmaxf(ev, lo), hi);
+  }
+}
+// clamp backward: pass where lo <= e <= hi; exp backward: * e
+__global__ void exp_clamp_bwd_k(const float* e, const float* g, long long n, float lo, float hi, float* gv) {
+  GRID_STRIDE(i, n) {
+    const float ev = e[i];
+    gv[i] = (ev >= lo && ev <= hi) ? g[i] * ev : 0.f;
+  }
+}
+
+// ---- reductions: partial[block] then one final block (fixed order) ----
+constexpr int RED_BLOCKS = 1024;
+
+template <int OP>
+__device__ __forceinline__ float red_term(const float* a, const float* b, long long i) {
+  if (OP == 0) {  // ce: clamp(-ln(p + 1e-10)/ln2, 0, 50)
+    const float t = -logf(a[i] + 1e-10f) / LN2F;
+    return fminf(fmaxf(t, 0.f), 50.f);
+  } else {  // squared error
+    const float d = a[i] - b[i];
+    return d * d;
+  }
+}
+
+template <int OP>
+__global__ void reduce_partial_k(const float* a, const float* b, long long n, float* part) {
+  __shared__ float lds[64];
+  float v[1] = {0.f};
+  GRID_STRIDE(i, n) v[0] += red_term<OP>(a, b, i);
+  block_sum<1>(v, lds);
+  if (threadIdx.x == 0) part[blockIdx.x] = v[0];
+}
+
+__global__ void reduce_final_k(const float* part, int nb, float scale, float* out) {
+  __shared__ float lds[64];
+  float v[1] = {0.f};
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) v[0] += part[i];
+  block_sum<1>(v, lds);
+  if (threadIdx.x == 0) out[0] = v[0] * scale;
+}
+
+int reduce_run(int op, const float* a, const float* b, long long n, float scale, float* out, void* ws,
+               size_t wsb, hipStream_t s) {
+  if (wsb < RED_BLOCKS * sizeof(float)) return IC_ERR_WORKSPACE;
+  float* part = (float*)ws;
+  long long nb = (n + 255) / 256;
+  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
+  if (nb < 1) nb = 1;
+  if (op == 0)
+    hipLaunchKernelGGL(reduce_partial_k<0>, dim3((unsigned)nb), dim3(256), 0, s, a, b, n, part);
+  else
+    hipLaunchKernelGGL(reduce_partial_k<1>, dim3((unsigned)nb), dim3(256), 0, s, a, b, n, part);
+  IC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_final_k, dim3(1), dim3(256), 0, s, part, (int)nb, scale, out);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+// torch: clamp(-1 * log(p + 1e-10) / LOG2, 0, 50): grad mask 0 <= t <= 50
+__global__ void ce_bwd_k(const float* p, const float* gout, long long n, float* gp) {
+  const float g = gout[0];
+  GRID_STRIDE(i, n) {
+    const float pe = p[i] + 1e-10f;
+    const float t = -logf(pe) / LN2F;
+    gp[i] = (t >= 0.f && t <= 50.f) ? g * (-1.f / (pe * LN2F)) : 0.f;
+  }
+}
+
+__global__ void mse_bwd_k(const float* a, const float* b, const float* gout, long long n, float* ga, float* gb) {
+  const float g = gout[0] * (2.f / (float)n);
+  GRID_STRIDE(i, n) {
+    const float d = (a[i] - b[i]) * g;
+    if (ga) ga[i] = d;
+    if (gb) gb[i] = -d;
+  }
+}
+
+__global__ void sqdiff_fwd_k(const float* a, const float* b, long long n, float* o) {
+  GRID_STRIDE(i, n) {
+    const float d = a[i] - b[i];
+    o[i] = d * d;
+  }
+}
+__global__ void sqdiff_bwd_k(const float* a, const float* b, const float* g, long long n, float* ga, float* gb) {
+  GRID_STRIDE(i, n) {
+    const float d = 2.f * (a[i] - b[i]) * g[i];
+    if (ga) ga[i] = d;
+    if (gb) gb[i] = -d;
+  }
+}
+
+__global__ void uniform_k(float* u, long long n, unsigned long long seed, unsigned long long off) {
+  GRID_STRIDE(i, n) u[i] = philox_uniform(seed, off + (unsigned long long)i);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ic_device_sync_check(void* stream) {
+  hipLaunchKernelGGL(uniform_k, dim3(1), dim3(64), 0, (hipStream_t)stream, (float*)nullptr, 0LL, 0ULL, 0ULL);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_nonneg_fwd(const float* p, long long n, float bound, float ped, float* out, void* stream) {
+  hipLaunchKernelGGL(nonneg_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, n, bound, ped, out);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_nonneg_bwd(const float* p, const float* gout, long long n, float bound, float* gin, void* stream) {
+  hipLaunchKernelGGL(nonneg_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gout, n, bound, gin);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_bound_fwd(const float* x, long long n, float bound, int upper, float* y, void* stream) {
+  hipLaunchKernelGGL(bound_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, bound, upper, y);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_bound_bwd(const float* x, const float* g, long long n, float bound, int upper, float* gx, void* stream) {
+  hipLaunchKernelGGL(bound_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, g, n, bound, upper, gx);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_relu_fwd(const float* x, long long n, float* y, void* stream) {
+  hipLaunchKernelGGL(relu_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, y);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_relu_bwd(const float* y, const float* g, long long n, float* gx, void* stream) {
+  hipLaunchKernelGGL(relu_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, y, g, n, gx);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_abs_fwd(const float* x, long long n, float* y, void* stream) {
+  hipLaunchKernelGGL(abs_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, y);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_abs_bwd(const float* x, const float* g, long long n, float* gx, void* stream) {
+  hipLaunchKernelGGL(abs_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, g, n, gx);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_exp_clamp_fwd(const float* v, long long n, float lo, float hi, float* sigma, float* e, void* stream) {
+  hipLaunchKernelGGL(exp_clamp_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, v, n, lo, hi, sigma, e);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_exp_clamp_bwd(const float* e, const float* g, long long n, float lo, float hi, float* gv, void* stream) {
+  hipLaunchKernelGGL(exp_clamp_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, e, g, n, lo, hi, gv);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+size_t ic_reduce_ws(long long n) { (void)n; return RED_BLOCKS * sizeof(float); }
+
+int ic_ce_loss_fwd(const float* p, long long n, float* out, void* ws, size_t ws_bytes, void* stream) {
+  return reduce_run(0, p, nullptr, n, 1.f, out, ws, ws_bytes, (hipStream_t)stream);
+}
+int ic_ce_loss_bwd(const float* p, const float* gout, long long n, float* gp, void* stream) {
+  hipLaunchKernelGGL(ce_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gout, n, gp);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_mse_fwd(const float* a, const float* b, long long n, float* out, void* ws, size_t ws_bytes, void* stream) {
+  return reduce_run(1, a, b, n, 1.f / (float)n, out, ws, ws_bytes, (hipStream_t)stream);
+}
+int ic_mse_bwd(const float* a, const float* b, const float* gout, long long n, float* ga, float* gb, void* stream) {
+  hipLaunchKernelGGL(mse_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, gout, n, ga, gb);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_sqdiff_fwd(const float* a, const float* b, long long n, float* out, void* stream) {
+  hipLaunchKernelGGL(sqdiff_fwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, n, out);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_sqdiff_bwd(const float* a, const float* b, const float* g, long long n, float* ga, float* gb, void* stream) {
+  hipLaunchKernelGGL(sqdiff_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, g, n, ga, gb);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset, void* stream) {
+  hipLaunchKernelGGL(uniform_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, u, n, seed, offset);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// Entropy bottleneck kernels (HBM/latency-bound elementwise work).
+//
+// factorized : modelling/blocks/entropy_model.py:47-114 (CDF MLP 1-3-3-3-1 per
+//              channel) and :204-269 (noise/round, sign-trick likelihood).
+//              One block per channel: the per-channel parameter gradients are
+//              block reductions in a fixed order (deterministic).
+// conditional: entropy_model.py:280-378, Laplacian (default) / Gaussian CDF.
+#include "../../include/imgcomp.h"
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float dsoftplusf(float x) { return x > 20.f ? 1.f : 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float signf_(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+struct ChanParams {
+  float sw0[3], b0[3], tf0[3];
+  float sw1[9], b1[3], tf1[3];
+  float sw2[9], b2[3], tf2[3];
+  float sw3[3], b3;
+};
+
+__device__ __forceinline__ void load_chan(const ic_fact_params& P, int c, ChanParams& q) {
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    q.sw0[o] = softplusf(P.w0[c * 3 + o]);
+    q.b0[o] = P.b0[c * 3 + o];
+    q.tf0[o] = tanhf(P.f0[c * 3 + o]);
+    q.b1[o] = P.b1[c * 3 + o];
+    q.tf1[o] = tanhf(P.f1[c * 3 + o]);
+    q.b2[o] = P.b2[c * 3 + o];
+    q.tf2[o] = tanhf(P.f2[c * 3 + o]);
+    q.sw3[o] = softplusf(P.w3[c * 3 + o]);
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    q.sw1[j] = softplusf(P.w1[c * 9 + j]);
+    q.sw2[j] = softplusf(P.w2[c * 9 + j]);
+  }
+  q.b3 = P.b3[c];
+}
+
+// activations of one MLP evaluation (pre-gate a*, post-gate h*)
+struct Acts {
+  float a0[3], h0[3], a1[3], h1[3], a2[3], h2[3];
+  float out;
+};
+
+__device__ __forceinline__ void mlp_fwd(const ChanParams& q, float v, Acts& A) {
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    A.a0[o] = q.sw0[o] * v + q.b0[o];
+    A.h0[o] = A.a0[o] + tanhf(A.a0[o]) * q.tf0[o];
+  }
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    A.a1[o] = q.sw1[o * 3 + 0] * A.h0[0] + q.sw1[o * 3 + 1] * A.h0[1] + q.sw1[o * 3 + 2] * A.h0[2] + q.b1[o];
+    A.h1[o] = A.a1[o] + tanhf(A.a1[o]) * q.tf1[o];
+  }
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    A.a2[o] = q.sw2[o * 3 + 0] * A.h1[0] + q.sw2[o * 3 + 1] * A.h1[1] + q.sw2[o * 3 + 2] * A.h1[2] + q.b2[o];
+    A.h2[o] = A.a2[o] + tanhf(A.a2[o]) * q.tf2[o];
+  }
+  A.out = q.sw3[0] * A.h2[0] + q.sw3[1] * A.h2[1] + q.sw3[2] * A.h2[2] + q.b3;
+}
+
+// gradient accumulators layout (43 floats):
+// [0..2] w0, [3..5] b0, [6..8] f0, [9..17] w1, [18..20] b1, [21..23] f1,
+// [24..32] w2, [33..35] b2, [36..38] f2, [39..41] w3, [42] b3
+constexpr int NG = 43;
+
+// backward of one evaluation with upstream g; accumulates "raw" gradients wrt
+// softplus(W) (converted to W by the caller once per channel) and returns dv.
+__device__ __forceinline__ float mlp_bwd(const ChanParams& q, float v, const Acts& A, float g, float (&G)[NG]) {
+  float dh2[3], da2[3], dh1[3], da1[3], dh0[3], da0[3];
+  // layer 3
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    G[39 + i] += g * A.h2[i];
+    dh2[i] = g * q.sw3[i];
+  }
+  G[42] += g;
+  // layer 2 gate
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    const float th = tanhf(A.a2[o]);
+    da2[o] = dh2[o] * (1.f + (1.f - th * th) * q.tf2[o]);
+    G[36 + o] += dh2[o] * th;  // * (1 - tf^2) applied by caller
+    G[33 + o] += da2[o];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dh1[i] = 0.f;
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      G[24 + o * 3 + i] += da2[o] * A.h1[i];
+      dh1[i] += q.sw2[o * 3 + i] * da2[o];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    const float th = tanhf(A.a1[o]);
+    da1[o] = dh1[o] * (1.f + (1.f - th * th) * q.tf1[o]);
+    G[21 + o] += dh1[o] * th;
+    G[18 + o] += da1[o];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dh0[i] = 0.f;
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      G[9 + o * 3 + i] += da1[o] * A.h0[i];
+      dh0[i] += q.sw1[o * 3 + i] * da1[o];
+    }
+  }
+  float dv = 0.f;
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    const float th = tanhf(A.a0[o]);
+    da0[o] = dh0[o] * (1.f + (1.f - th * th) * q.tf0[o]);
+    G[6 + o] += dh0[o] * th;
+    G[3 + o] += da0[o];
+    G[0 + o] += da0[o] * v;
+    dv += q.sw0[o] * da0[o];
+  }
+  return dv;
+}
+
+__device__ __forceinline__ float quant(float x, int mode, const float* u, long long i,
+                                       unsigned long long seed, unsigned long long off) {
+  if (mode == 1) return rintf(x);
+  const float uu = mode == 0 ? u[i] : philox_uniform(seed, off + (unsigned long long)i);
+  return x + (uu - 0.5f);
+}
+
+__global__ void fact_fwd_k(const float* z, long long n, int C, const ic_fact_params P, int mode,
+                           const float* u, unsigned long long seed, unsigned long long off, float* qo,
+                           float* po) {
+  const int c = blockIdx.x;
+  ChanParams q;
+  load_chan(P, c, q);
+  const long long ne = n / C;
+  for (long long e = threadIdx.x; e < ne; e += blockDim.x) {
+    const long long i = e * C + c;
+    const float qv = quant(z[i], mode, u, i, seed, off);
+    qo[i] = qv;
+    Acts lo, up;
+    mlp_fwd(q, qv - 0.5f, lo);
+    mlp_fwd(q, qv + 0.5f, up);
+    const float s = -signf_(lo.out + up.out);
+    po[i] = s * (sigmoidf_(up.out * s) - sigmoidf_(lo.out * s));
+  }
+}
+
+__global__ void fact_bwd_k(const float* qin, long long n, int C, const ic_fact_params P,
+                           const float* dq, const float* dp, float* dz, const ic_fact_grads GR, int round_mode) {
+  __shared__ float lds[16 * NG];
+  const int c = blockIdx.x;
+  ChanParams q;
+  load_chan(P, c, q);
+  float G[NG];
+#pragma unroll
+  for (int j = 0; j < NG; ++j) G[j] = 0.f;
+  const long long ne = n / C;
+  for (long long e = threadIdx.x; e < ne; e += blockDim.x) {
+    const long long i = e * C + c;
+    const float qv = qin[i];
+    float dqv = 0.f;
+    const float gp = dp ? dp[i] : 0.f;
+    if (gp != 0.f) {
+      Acts lo, up;
+      mlp_fwd(q, qv - 0.5f, lo);
+      mlp_fwd(q, qv + 0.5f, up);
+      const float s = -signf_(lo.out + up.out);
+      const float su = sigmoidf_(s * up.out), sl = sigmoidf_(s * lo.out);
+      // p = s*(sig(s*up) - sig(s*lo)), s detached
+      const float gup = gp * s * su * (1.f - su) * s;
+      const float glo = -gp * s * sl * (1.f - sl) * s;
+      dqv += mlp_bwd(q, qv + 0.5f, up, gup, G);
+      dqv += mlp_bwd(q, qv - 0.5f, lo, glo, G);
+    }
+    if (dz) dz[i] = round_mode ? 0.f : (dq ? dq[i] : 0.f) + dqv;
+  }
+  block_sum<NG>(G, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float w0 = P.w0[c * 3 + o], w3 = P.w3[c * 3 + o];
+      GR.w0[c * 3 + o] = G[0 + o] * dsoftplusf(w0);
+      GR.b0[c * 3 + o] = G[3 + o];
+      const float t0 = tanhf(P.f0[c * 3 + o]);
+      GR.f0[c * 3 + o] = G[6 + o] * (1.f - t0 * t0);
+      GR.b1[c * 3 + o] = G[18 + o];
+      const float t1 = tanhf(P.f1[c * 3 + o]);
+      GR.f1[c * 3 + o] = G[21 + o] * (1.f - t1 * t1);
+      GR.b2[c * 3 + o] = G[33 + o];
+      const float t2 = tanhf(P.f2[c * 3 + o]);
+      GR.f2[c * 3 + o] = G[36 + o] * (1.f - t2 * t2);
+      GR.w3[c * 3 + o] = G[39 + o] * dsoftplusf(w3);
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      GR.w1[c * 9 + j] = G[9 + j] * dsoftplusf(P.w1[c * 9 + j]);
+      GR.w2[c * 9 + j] = G[24 + j] * dsoftplusf(P.w2[c * 9 + j]);
+    }
+    GR.b3[c] = G[42];
+  }
+}
+
+// ---------------------------------------------------------------- conditional
+__device__ __forceinline__ float cdf_lap(float v) {
+  return 0.5f - 0.5f * signf_(v) * expm1f(-fabsf(v));
+}
+__device__ __forceinline__ float dcdf_lap(float v) {
+  const float sg = signf_(v);
+  return 0.5f * sg * sg * (expm1f(-fabsf(v)) + 1.f);
+}
+constexpr float RSQRT2 = 0.70710678118654752f;
+constexpr float TWO_OVER_SQRTPI = 1.12837916709551257f;
+__device__ __forceinline__ float cdf_gauss(float v) { return 0.5f * (1.f + erff(v * 1.0f * RSQRT2)); }
+__device__ __forceinline__ float dcdf_gauss(float v) {
+  const float t = v * RSQRT2;
+  return 0.5f * TWO_OVER_SQRTPI * expf(-t * t) * RSQRT2;
+}
+
+__global__ void cond_fwd_k(const float* y, const float* sc, const float* mean, long long n, int kind, int mode,
+                           const float* u, unsigned long long seed, unsigned long long off, float* qo, float* po) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float qv = quant(y[i], mode, u, i, seed, off);
+    qo[i] = qv;
+    const float a = fabsf(qv - (mean ? mean[i] : 0.f));
+    const float s = sc[i];
+    const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
+    po[i] = kind == 0 ? cdf_lap(vu) - cdf_lap(vl) : cdf_gauss(vu) - cdf_gauss(vl);
+  }
+}
+
+__global__ void cond_bwd_k(const float* q, const float* sc, const float* mean, long long n, int kind,
+                           const float* dq, const float* dp, float* dy, float* ds, float* dm) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float d = q[i] - (mean ? mean[i] : 0.f);
+    const float a = fabsf(d);
+    const float s = sc[i];
+    const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
+    const float g = dp ? dp[i] : 0.f;
+    const float fu = kind == 0 ? dcdf_lap(vu) : dcdf_gauss(vu);
+    const float fl = kind == 0 ? dcdf_lap(vl) : dcdf_gauss(vl);
+    const float gvu = g * fu, gvl = -g * fl;   // dL/dvu, dL/dvl
+    const float ga = -(gvu + gvl) / s;         // dv/da = -1/s for both
+    const float gs = -(gvu * vu + gvl * vl) / s;
+    const float gd = ga * signf_(d);
+    if (dy) dy[i] = (dq ? dq[i] : 0.f) + gd;
+    if (ds) ds[i] = gs;
+    if (dm) dm[i] = -gd;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ic_factorized_fwd(const float* z, long long n, int C, const ic_fact_params* prm, int mode, const float* u,
+                      unsigned long long seed, unsigned long long offset, float* q, float* p, void* stream) {
+  if (C <= 0 || n % C != 0 || (mode == 0 && !u)) return IC_ERR_ARG;
+  hipLaunchKernelGGL(fact_fwd_k, dim3(C), dim3(256), 0, (hipStream_t)stream, z, n, C, *prm, mode, u, seed,
+                     offset, q, p);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* prm, const float* dq,
+                      const float* dp, float* dz, const ic_fact_grads* grd, void* stream) {
+  if (C <= 0 || n % C != 0) return IC_ERR_ARG;
+  hipLaunchKernelGGL(fact_bwd_k, dim3(C), dim3(256), 0, (hipStream_t)stream, q, n, C, *prm, dq, dp, dz, *grd, 0);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_conditional_fwd(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
+                       const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                       void* stream) {
+  if (mode == 0 && !u) return IC_ERR_ARG;
+  long long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(cond_fwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, y, scale, mean, n, kind,
+                     mode, u, seed, offset, q, p);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_conditional_bwd(const float* q, const float* scale, const float* mean, long long n, int kind,
+                       const float* dq, const float* dp, float* dy, float* dscale, float* dmean, void* stream) {
+  long long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(cond_bwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, q, scale, mean, n, kind,
+                     dq, dp, dy, dscale, dmean);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+// Internal descriptors of the two gather-GEMM kernel families.
+//
+//  (1) ig_*  "implicit GEMM" output-stationary convolution:
+//        out[m][n] = sum_k A[m][k] * Bt[n][k]
+//      m = output grid pixel (img, gy, gx) of one sub-pixel phase,
+//      k = (tap t, input channel c); A[m][(t,c)] = x[img, gy*s+dy_t, gx*s+dx_t, c]
+//      (zero outside the image), Bt = packed weights [T][Npad][Cin].
+//      A stride-s transposed conv (= conv dgrad) is up to s*s phases, each a
+//      dense stride-1 gather conv with 2..3 x 2..3 taps (no zero stuffing).
+//  (2) wg_*  weight gradient (split-K over pixels):
+//        dW[g][(t,c)] = sum_p G[p][g] * X[p*s + d_t][c]
+#pragma once
+#include "common.h"
+
+enum IgEpilogue {
+  EPI_NONE = 0,
+  EPI_RELU = 1,
+  EPI_GDN = 2,        // y = aux0 / sqrt(v),  aux_out = v (norm)
+  EPI_IGDN = 3,       // y = aux0 * sqrt(v),  aux_out = v
+  EPI_GDN_BWD = 4,    // y = aux2 / sqrt(aux1) + 2*aux0*v
+  EPI_IGDN_BWD = 5    // y = aux2 * sqrt(aux1) + 2*aux0*v
+};
+enum IgAOp { AOP_NONE = 0, AOP_SQUARE = 1, AOP_ABS = 2 };
+
+struct IgPhase {
+  const float* wp;  // fast: [T][Npad][Cin]; generic: [Npad][Kpad]
+  int T;
+  int Hg, Wg;       // output grid of this phase
+  int oys, oxs, oy0, ox0;  // output pixel = (gy*oys+oy0, gx*oxs+ox0)
+  int mtiles;
+  long long m_off;  // row offset of this phase inside the split-K partial buffer
+  FastDiv fd_hw, fd_w;  // divide by Hg*Wg and by Wg
+  int dy[IC_MAXT], dx[IC_MAXT];
+};
+
+struct IgDesc {
+  const float* x;
+  long long xs_n, xs_h, xs_w, xs_c;
+  int Hx, Wx, Cin;
+  int N, stride;
+  int Cout, Npad, Kc;  // Kc: fast = Cin, generic = Kpad (T*Cin rounded up to 32)
+  int generic;
+  float* y;
+  long long ys_n, ys_h, ys_w, ys_c;
+  const float* bias;
+  int epi, a_op;
+  const float* aux0;
+  const float* aux1;
+  const float* aux2;
+  float* aux_out;
+  int nphase;
+  int ksplit, kcps;  // K splits and K-chunks (of 32) per split
+  float* partial;    // [ksplit][Mtot][Cout]
+  long long Mtot;
+  int bm, bn;        // chosen tile (set by ig_plan)
+  IgPhase ph[IC_MAXPH];
+};
+
+// Fill tile choice, mtiles, split-K; returns partial-buffer bytes needed.
+size_t ig_plan(IgDesc& d);
+int ig_run(IgDesc& d, hipStream_t s);
+// N padding the packed-weight layout must use for `Cout`
+int ig_npad(int Cout);
+
+struct WgDesc {
+  const float* g;
+  long long gs_n, gs_h, gs_w, gs_c;
+  int Hg, Wg, Cg;
+  const float* x;
+  long long xs_n, xs_h, xs_w, xs_c;
+  int Hx, Wx, Cx;
+  int N, stride, T;
+  int x_op;        // AOP_SQUARE -> x^2
+  int g_vec;       // G rows channel-contiguous (float4 loads)
+  int generic;     // columns = (t, c) flattened
+  int ncols;       // fast: Cx ; generic: T*Cx
+  int bm, bn;
+  int mtiles, ntiles;
+  long long P;     // N*Hg*Wg
+  int pps, nsplit; // pixels per split, number of splits
+  float* partial;  // [nsplit][Tp][Cg][ncols]
+  int dy[IC_MAXT], dx[IC_MAXT];
+};
+
+size_t wg_plan(WgDesc& d);
+int wg_run(WgDesc& d, hipStream_t s);
+// out[g][c][kk(t)] (+)= sum over splits; kk_of_t maps tap -> ky*k+kx, kk = k*k
+int wg_reduce(const WgDesc& d, float* out, const int* kk_of_t, int kk, hipStream_t s);
+
+// column sums: out[c] = scale * sum over pixels of t[n,c,h,w]
+size_t colsum_ws(long long rows, int C);
+int colsum(const float* t, long long s_n, long long s_c, long long s_h, long long s_w,
+           int N, int C, int H, int W, float* out, float scale, void* ws, hipStream_t s);
+
+// weight packing
+//  mode 0 (direct):     wp[t][a][b]   = W[a][b][ky_t][kx_t]   (out ch a, reduce b)
+//  mode 1 (transposed): wp[t][b][a]   = W[a][b][ky_t][kx_t]   (out ch b, reduce a)
+//  generic: the (t, reduce-ch) pair is flattened into a Kpad-long row.
+int pack_weights(const float* W, int A, int B, int k, int mode, int generic,
+                 int T, const int* ky, const int* kx, int Npad, int Kpad,
+                 float* wp, hipStream_t s);

@@ -1,0 +1,336 @@
+// Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), gfx950.
+//
+// Block = 256 threads = 4 waves; block tile BM (pixels) x BN (out channels);
+// wave tile WM x WN made of 32x32 MFMA tiles.  K is walked in chunks of 32
+// (one tap x 32 input channels on the fast path), register-staged into a
+// single LDS image per operand ([rows][36]-float rows: 16-B aligned and
+// conflict-free for the ds_read_b128 fragment reads below).
+//
+// K permutation: inside a 32-chunk, MFMA step (q,s) of lane-half h consumes
+// logical k = 16h + 4q + s for BOTH operands, so each lane's 16 operand values
+// per chunk are contiguous in LDS -> 4 x ds_read_b128 per operand tile.
+#include "gemm.h"
+
+namespace {
+
+constexpr int LDK = 36;
+
+__device__ __forceinline__ void ig_store_out(const IgDesc& d, float v, uint32_t yoff, int n) {
+  if (d.bias) v += d.bias[n];
+  switch (d.epi) {
+    case EPI_RELU:
+      v = v > 0.f ? v : 0.f;
+      break;
+    case EPI_GDN: {
+      const float xv = d.aux0[yoff];
+      d.aux_out[yoff] = v;
+      v = xv / sqrtf(v);
+      break;
+    }
+    case EPI_IGDN: {
+      const float xv = d.aux0[yoff];
+      d.aux_out[yoff] = v;
+      v = xv * sqrtf(v);
+      break;
+    }
+    case EPI_GDN_BWD: {
+      const float xv = d.aux0[yoff], nr = d.aux1[yoff], g = d.aux2[yoff];
+      v = g / sqrtf(nr) + 2.f * xv * v;
+      break;
+    }
+    case EPI_IGDN_BWD: {
+      const float xv = d.aux0[yoff], nr = d.aux1[yoff], g = d.aux2[yoff];
+      v = g * sqrtf(nr) + 2.f * xv * v;
+      break;
+    }
+    default:
+      break;
+  }
+  d.y[yoff] = v;
+}
+
+__device__ __forceinline__ uint32_t ig_out_offset(const IgDesc& d, const IgPhase& P, uint32_t m) {
+  const uint32_t img = fdiv(m, P.fd_hw);
+  const uint32_t rem = m - img * (uint32_t)P.fd_hw.d;
+  const uint32_t gy = fdiv(rem, P.fd_w);
+  const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+  const uint32_t oy = gy * P.oys + P.oy0, ox = gx * P.oxs + P.ox0;
+  return img * (uint32_t)d.ys_n + oy * (uint32_t)d.ys_h + ox * (uint32_t)d.ys_w;
+}
+
+__device__ __forceinline__ float aop(int op, float v) {
+  return op == AOP_SQUARE ? v * v : (op == AOP_ABS ? fabsf(v) : v);
+}
+
+template <int BM, int BN, int WM, int WN, bool GEN>
+__global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int APASS = BM / 32, BPASS = BN / 32;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  __shared__ __attribute__((aligned(16))) float As[BM * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * LDK];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  if ((int)blockIdx.x >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = GEN ? (d.Kc >> 5) : P.T * (d.Cin >> 5);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x;
+  const int lrow = tid >> 3, lc4 = tid & 7;
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+
+  // per-pass gather origin: pixel offset (32-bit) and input row/col of tap (0,0)
+  uint32_t a_off[APASS];
+  int a_iy[APASS], a_ix[APASS];
+#pragma unroll
+  for (int p = 0; p < APASS; ++p) {
+    const uint32_t m = m0 + lrow + 32 * p;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[p] = ok ? (int)gy * d.stride : -0x40000000;  // invalid rows fail the bounds test
+    a_ix[p] = (int)gx * d.stride;
+    a_off[p] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[p] * xsh + (uint32_t)a_ix[p] * xsw;
+  }
+  const float* __restrict__ xg = d.x;
+
+  floatx4v ra[APASS], rb[BPASS];
+
+#define IG_GLOAD(c_)                                                                              \
+  do {                                                                                            \
+    const int c__ = (c_);                                                                         \
+    if constexpr (!GEN) {                                                                         \
+      const int cpt = d.Cin >> 5;                                                                 \
+      const int t = c__ / cpt, cc = c__ - t * cpt;                                                \
+      const int dy = P.dy[t], dx = P.dx[t];                                                       \
+      const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);         \
+      _Pragma("unroll") for (int p = 0; p < APASS; ++p) {                                         \
+        const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;                                           \
+        floatx4v v = {0.f, 0.f, 0.f, 0.f};                                                        \
+        if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)                       \
+          v = *(const floatx4v*)(xg + (a_off[p] + toff));                                         \
+        if (d.a_op) { v[0] = aop(d.a_op, v[0]); v[1] = aop(d.a_op, v[1]); v[2] = aop(d.a_op, v[2]); v[3] = aop(d.a_op, v[3]); } \
+        ra[p] = v;                                                                                \
+      }                                                                                           \
+      const float* wb = P.wp + ((size_t)t * d.Npad + n0 + lrow) * d.Cin + cc * 32 + lc4 * 4;      \
+      _Pragma("unroll") for (int p = 0; p < BPASS; ++p)                                           \
+        rb[p] = *(const floatx4v*)(wb + (size_t)(32 * p) * d.Cin);                                  \
+    } else {                                                                                      \
+      _Pragma("unroll") for (int p = 0; p < APASS; ++p) {                                         \
+        float v4[4];                                                                              \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                           \
+          const int k = c__ * 32 + lc4 * 4 + e;                                                   \
+          const int t = k / d.Cin, ci = k - t * d.Cin;                                            \
+          float val = 0.f;                                                                        \
+          if (t < P.T) {                                                                          \
+            const int dy = P.dy[t], dx = P.dx[t];                                                 \
+            const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;                                       \
+            if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)                   \
+              val = aop(d.a_op, xg[a_off[p] + (uint32_t)(dy * (int)xsh + dx * (int)xsw) +         \
+                                   (uint32_t)ci * (uint32_t)d.xs_c]);                             \
+          }                                                                                       \
+          v4[e] = val;                                                                            \
+        }                                                                                         \
+        ra[p] = floatx4v{v4[0], v4[1], v4[2], v4[3]};                                          \
+      }                                                                                           \
+      const float* wb = P.wp + (size_t)(n0 + lrow) * d.Kc + c__ * 32 + lc4 * 4;                   \
+      _Pragma("unroll") for (int p = 0; p < BPASS; ++p)                                           \
+        rb[p] = *(const floatx4v*)(wb + (size_t)(32 * p) * d.Kc);                                   \
+    }                                                                                             \
+  } while (0)
+
+#define IG_SSTORE()                                                                               \
+  do {                                                                                            \
+    _Pragma("unroll") for (int p = 0; p < APASS; ++p)                                             \
+      *(floatx4v*)&As[(lrow + 32 * p) * LDK + lc4 * 4] = ra[p];                                     \
+    _Pragma("unroll") for (int p = 0; p < BPASS; ++p)                                             \
+      *(floatx4v*)&Bs[(lrow + 32 * p) * LDK + lc4 * 4] = rb[p];                                     \
+  } while (0)
+
+  const int lane = tid & 63, w = tid >> 6;
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 31, h = lane >> 5;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (cb < ce) {
+    IG_GLOAD(cb);
+    IG_SSTORE();
+  }
+  __syncthreads();
+  const float* Ard = &As[(wm * WM + r) * LDK + 16 * h];
+  const float* Brd = &Bs[(wn * WN + r) * LDK + 16 * h];
+  for (int c = cb; c < ce; ++c) {
+    if (c + 1 < ce) IG_GLOAD(c + 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      floatx4v a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const floatx4v*)(Ard + i * 32 * LDK + 4 * q);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const floatx4v*)(Brd + j * 32 * LDK + 4 * q);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][2], b[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][3], b[j][3], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (c + 1 < ce) IG_SSTORE();
+    __syncthreads();
+  }
+#undef IG_GLOAD
+#undef IG_SSTORE
+
+  // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (reg&3)+8*(reg>>2)+4*(lane>>5)
+  if (d.ksplit > 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m >= M) continue;
+        float* prow = d.partial + ((size_t)split * d.Mtot + P.m_off + m) * d.Cout;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WN + j * 32 + r;
+          if (n < d.Cout) prow[n] = acc[i][j][reg];
+        }
+      }
+    return;
+  }
+  const uint32_t ysc = (uint32_t)d.ys_c;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (m >= M) continue;
+      const uint32_t ob = ig_out_offset(d, P, m);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 32 + r;
+        if (n < d.Cout) ig_store_out(d, acc[i][j][reg], ob + (uint32_t)n * ysc, n);
+      }
+    }
+}
+
+// split-K reduction + epilogue: one thread per (row, channel)
+__global__ void ig_reduce_kernel(const IgDesc d) {
+  const long long total = d.Mtot * d.Cout;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long mg = i / d.Cout;
+    const int n = (int)(i - mg * d.Cout);
+    float v = 0.f;
+    for (int s = 0; s < d.ksplit; ++s) v += d.partial[((long long)s * d.Mtot + mg) * d.Cout + n];
+    int ph = 0;
+#pragma unroll
+    for (int q = 1; q < IC_MAXPH; ++q)
+      if (q < d.nphase && mg >= d.ph[q].m_off) ph = q;
+    const IgPhase& P = d.ph[ph];
+    const uint32_t m = (uint32_t)(mg - P.m_off);
+    ig_store_out(d, v, ig_out_offset(d, P, m) + (uint32_t)n * (uint32_t)d.ys_c, n);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int ig_launch_t(const IgDesc& d, hipStream_t s) {
+  int mt = 0;
+  for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
+  dim3 grid(mt, d.Npad / BN, d.nphase * d.ksplit);
+  if (d.generic)
+    hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
+  else
+    hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+}  // namespace
+
+int ig_npad(int Cout) {
+  if (Cout % 192 == 0) return Cout;
+  if (Cout >= 64) return (Cout + 63) / 64 * 64;
+  return (Cout + 31) / 32 * 32;
+}
+
+size_t ig_plan(IgDesc& d) {
+  if (d.Cout % 192 == 0) { d.bm = 128; d.bn = 192; }
+  else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
+  else { d.bm = 256; d.bn = 32; }
+  d.Npad = ig_npad(d.Cout);
+  long long mtot = 0;
+  long long tiles = 0;
+  int nchunks_max = 0;
+  for (int p = 0; p < d.nphase; ++p) {
+    IgPhase& P = d.ph[p];
+    const long long M = (long long)d.N * P.Hg * P.Wg;
+    P.mtiles = ic_cdiv(M, d.bm);
+    P.fd_hw = make_fastdiv((uint32_t)((long long)P.Hg * P.Wg));
+    P.fd_w = make_fastdiv((uint32_t)P.Wg);
+    P.m_off = mtot;
+    mtot += M;
+    tiles += (long long)P.mtiles * (d.Npad / d.bn);
+    const int nch = d.generic ? (d.Kc >> 5) : P.T * (d.Cin >> 5);
+    nchunks_max = nch > nchunks_max ? nch : nchunks_max;
+  }
+  d.Mtot = mtot;
+  // split K when the tile grid cannot fill 256 CUs x 2 blocks
+  int ksplit = 1;
+  if (tiles < 512 && nchunks_max >= 4) {
+    ksplit = (int)((1024 + tiles - 1) / tiles);
+    const int maxs = nchunks_max / 2;
+    if (ksplit > maxs) ksplit = maxs;
+    if (ksplit < 1) ksplit = 1;
+  }
+  d.kcps = (nchunks_max + ksplit - 1) / ksplit;
+  d.ksplit = (nchunks_max + d.kcps - 1) / d.kcps;
+  if (d.ksplit <= 1) {
+    d.ksplit = 1;
+    d.kcps = nchunks_max;
+    return 0;
+  }
+  return (size_t)d.ksplit * (size_t)mtot * (size_t)d.Cout * sizeof(float);
+}
+
+int ig_run(IgDesc& d, hipStream_t s) {
+  if (d.Mtot == 0) return IC_OK;
+  if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
+  if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
+  int rc;
+  if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
+  else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);
+  else rc = ig_launch_t<256, 32, 64, 32>(d, s);
+  if (rc) return rc;
+  if (d.ksplit > 1) {
+    const long long total = d.Mtot * d.Cout;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(ig_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d);
+    IC_CHECK_LAUNCH();
+  }
+  return IC_OK;
+}

@@ -1,0 +1,60 @@
+// Weight re-packing for the implicit-GEMM kernels (per call; weights change
+// every optimizer step).  PyTorch layout W[a][b][ky][kx] ->
+//   direct     : out channel a, reduce channel b
+//   transposed : out channel b, reduce channel a
+//   fast       : wp[t][n][r]          (n < Npad, zero rows for n >= Nout)
+//   generic    : wp[n][t*R + r]       (row padded with zeros to Kpad)
+#include "gemm.h"
+
+namespace {
+struct PackArgs {
+  const float* W;
+  float* wp;
+  int A, B, k, mode, generic, T, Npad, Kpad;
+  int ky[IC_MAXT], kx[IC_MAXT];
+};
+
+__global__ void pack_kernel(const PackArgs p) {
+  const int Nout = p.mode == 0 ? p.A : p.B;
+  const int R = p.mode == 0 ? p.B : p.A;
+  const long long total = p.generic ? (long long)p.Npad * p.Kpad : (long long)p.T * p.Npad * R;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int t, n, r;
+    if (p.generic) {
+      n = (int)(i / p.Kpad);
+      const int kf = (int)(i - (long long)n * p.Kpad);
+      t = kf / R;
+      r = kf - t * R;
+    } else {
+      r = (int)(i % R);
+      const long long tn = i / R;
+      n = (int)(tn % p.Npad);
+      t = (int)(tn / p.Npad);
+    }
+    float v = 0.f;
+    if (n < Nout && t < p.T) {
+      const int a = p.mode == 0 ? n : r;
+      const int b = p.mode == 0 ? r : n;
+      v = p.W[(((long long)a * p.B + b) * p.k + p.ky[t]) * p.k + p.kx[t]];
+    }
+    p.wp[i] = v;
+  }
+}
+}  // namespace
+
+int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int T, const int* ky,
+                 const int* kx, int Npad, int Kpad, float* wp, hipStream_t s) {
+  if (T > IC_MAXT || T < 1) return IC_ERR_ARG;
+  PackArgs p;
+  p.W = W; p.wp = wp; p.A = A; p.B = B; p.k = k; p.mode = mode; p.generic = generic; p.T = T;
+  p.Npad = Npad; p.Kpad = Kpad;
+  for (int t = 0; t < T; ++t) { p.ky[t] = ky[t]; p.kx[t] = kx[t]; }
+  const int R = mode == 0 ? B : A;
+  const long long total = generic ? (long long)Npad * Kpad : (long long)T * Npad * R;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}

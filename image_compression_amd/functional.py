@@ -1,0 +1,600 @@
+"""Autograd functions over the HIP kernels of libimgcomp.so.
+
+Every forward/backward here launches hand-written gfx950 kernels through the
+C ABI (include/imgcomp.h) on torch's current stream.  PyTorch provides only
+allocation (caching allocator), stream handles and the autograd graph.
+There is deliberately no CPU / eager fallback: CPU tensors raise.
+
+Layout convention: activations with >= 32 channels live in NHWC
+(torch.channels_last) so every GEMM operand row is channel-contiguous; the
+3-channel image tensors stay NCHW and take the generic gather path.
+"""
+import ctypes
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from . import noise as _noise
+
+CL = torch.channels_last
+
+
+def _L():
+    return _lib.load()
+
+
+def _cl(t):
+    """Channels-last (NHWC) dense view/copy for GEMM operands with many channels."""
+    if t.shape[1] >= 32 and t.stride(1) != 1:
+        return t.contiguous(memory_format=CL)
+    if not (t.is_contiguous() or t.is_contiguous(memory_format=CL)):
+        return t.contiguous()
+    return t
+
+
+def _new_act(N, C, H, W, device):
+    if C >= 32:
+        return torch.empty((N, C, H, W), device=device, dtype=torch.float32, memory_format=CL)
+    return torch.empty((N, C, H, W), device=device, dtype=torch.float32)
+
+
+def _is_dense(t):
+    """Non-overlapping and dense storage in some dimension order."""
+    if t.numel() <= 1:
+        return True
+    expect = 1
+    for s, n in sorted((s, n) for s, n in zip(t.stride(), t.shape) if n != 1):
+        if s != expect:
+            return False
+        expect *= n
+    return True
+
+
+def _dense(t):
+    if t.is_contiguous() or _is_dense(t):
+        return t
+    return t.contiguous()
+
+
+def _match(g, ref):
+    """Return g with exactly ref's strides (elementwise kernels index storage)."""
+    if g.shape == ref.shape and g.stride() == ref.stride() and _is_dense(g):
+        return g
+    out = torch.empty_like(ref)
+    out.copy_(g)
+    return out
+
+
+def _ws(nbytes, device):
+    return _lib.workspace(nbytes, device)
+
+
+def _n(t):
+    return ctypes.c_longlong(t.numel())
+
+
+# ============================================================== convolutions
+class Conv2dFn(Function):
+    """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, act):
+        _lib.require_device(x, weight, bias)
+        L = _L()
+        x = _cl(x)
+        w = weight.contiguous()
+        b = None if bias is None else bias.contiguous()
+        N, Cin, H, W = x.shape
+        Cout, Cin_w, k, k2 = w.shape
+        if Cin_w != Cin or k != k2:
+            raise RuntimeError(f"conv2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
+        Ho = (H + 2 * padding - k) // stride + 1
+        Wo = (W + 2 * padding - k) // stride + 1
+        y = _new_act(N, Cout, Ho, Wo, x.device)
+        ax, ay = _lib.act(x), _lib.act(y)
+        nb = L.ic_conv2d_fwd_ws(ax, k, stride, padding, ay)
+        buf = _ws(nb, x.device)
+        _lib.check(L.ic_conv2d_fwd(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
+                                   _lib.ptr(buf), nb, _lib.stream_of(x)), "conv2d_fwd")
+        ctx.conf = (stride, padding, k, act, b is not None)
+        ctx.save_for_backward(x, w, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        stride, padding, k, act, has_b = ctx.conf
+        L = _L()
+        if act:
+            gy = relu_bwd(y, gy)
+        gy = _cl(gy)
+        dx = dw = db = None
+        st = _lib.stream_of(gy)
+        if ctx.needs_input_grad[0]:
+            dx = _new_act(*x.shape, x.device)
+            if x.stride(1) == 1 and dx.stride(1) != 1:
+                dx = dx.contiguous(memory_format=CL)
+            ag, adx = _lib.act(gy), _lib.act(dx)
+            nb = L.ic_conv2d_dgrad_ws(ag, k, stride, padding, adx)
+            buf = _ws(nb, gy.device)
+            _lib.check(L.ic_conv2d_dgrad(ag, _lib.ptr(w), k, stride, padding, adx, _lib.ptr(buf), nb, st),
+                       "conv2d_dgrad")
+        if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
+            dw = torch.empty_like(w)
+            db = torch.empty(w.shape[0], device=w.device, dtype=w.dtype) if has_b else None
+            ax, ag = _lib.act(x), _lib.act(gy)
+            nb = L.ic_conv2d_wgrad_ws(ax, ag, k, stride, padding)
+            buf = _ws(nb, gy.device)
+            _lib.check(L.ic_conv2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
+                                         _lib.ptr(buf), nb, st), "conv2d_wgrad")
+        return dx, dw, db, None, None, None
+
+
+class ConvTranspose2dFn(Function):
+    """torch.nn.ConvTranspose2d forward/backward (synthesis.py:55-57, prior_synthesis.py:54-56).
+    output_padding is implied by `out_hw`."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, act):
+        _lib.require_device(x, weight, bias)
+        L = _L()
+        x = _cl(x)
+        w = weight.contiguous()
+        b = None if bias is None else bias.contiguous()
+        N, Cin, H, W = x.shape
+        Cin_w, Cout, k, k2 = w.shape
+        if Cin_w != Cin or k != k2:
+            raise RuntimeError(f"conv_transpose2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
+        Ho = (H - 1) * stride - 2 * padding + k + output_padding
+        Wo = (W - 1) * stride - 2 * padding + k + output_padding
+        y = _new_act(N, Cout, Ho, Wo, x.device)
+        ax, ay = _lib.act(x), _lib.act(y)
+        nb = L.ic_conv_transpose2d_fwd_ws(ax, k, stride, padding, ay)
+        buf = _ws(nb, x.device)
+        _lib.check(L.ic_conv_transpose2d_fwd(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
+                                             _lib.ptr(buf), nb, _lib.stream_of(x)), "conv_transpose2d_fwd")
+        ctx.conf = (stride, padding, k, act, b is not None)
+        ctx.save_for_backward(x, w, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        stride, padding, k, act, has_b = ctx.conf
+        L = _L()
+        if act:
+            gy = relu_bwd(y, gy)
+        gy = _cl(gy)
+        dx = dw = db = None
+        st = _lib.stream_of(gy)
+        if ctx.needs_input_grad[0]:
+            dx = _new_act(*x.shape, x.device)
+            ag, adx = _lib.act(gy), _lib.act(dx)
+            nb = L.ic_conv_transpose2d_dgrad_ws(ag, k, stride, padding, adx)
+            buf = _ws(nb, gy.device)
+            _lib.check(L.ic_conv_transpose2d_dgrad(ag, _lib.ptr(w), k, stride, padding, adx, _lib.ptr(buf),
+                                                   nb, st), "conv_transpose2d_dgrad")
+        if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
+            dw = torch.empty_like(w)
+            db = torch.empty(w.shape[1], device=w.device, dtype=w.dtype) if has_b else None
+            ax, ag = _lib.act(x), _lib.act(gy)
+            nb = L.ic_conv_transpose2d_wgrad_ws(ax, ag, k, stride, padding)
+            buf = _ws(nb, gy.device)
+            _lib.check(L.ic_conv_transpose2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
+                                                   _lib.ptr(buf), nb, st), "conv_transpose2d_wgrad")
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, act=0):
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), int(act))
+
+
+def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, act=0):
+    return ConvTranspose2dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), int(act))
+
+
+# ============================================================== GDN
+class GDNFn(Function):
+    """modelling/layers/gdn.py:84-86 given re-parameterised gamma (C,C,1,1), beta (C,)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, inverse):
+        _lib.require_device(x, gamma, beta)
+        L = _L()
+        x = _cl(x)
+        g = gamma.contiguous()
+        b = beta.contiguous()
+        y = torch.empty_like(x)
+        norm = torch.empty_like(x)
+        ax, ay = _lib.act(x), _lib.act(y)
+        nb = L.ic_gdn_fwd_ws(ax)
+        buf = _ws(nb, x.device)
+        _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(b), int(inverse), ay, _lib.ptr(norm), _lib.ptr(buf),
+                                nb, _lib.stream_of(x)), "gdn_fwd")
+        ctx.inverse = int(inverse)
+        ctx.save_for_backward(x, norm, g)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, norm, g = ctx.saved_tensors
+        L = _L()
+        gy = _match(gy, x)
+        dx = torch.empty_like(x)
+        dg = torch.empty_like(g)
+        dbeta = torch.empty(g.shape[0], device=g.device, dtype=g.dtype)
+        ax, adx = _lib.act(x), _lib.act(dx)
+        nb = L.ic_gdn_bwd_ws(ax)
+        buf = _ws(nb, x.device)
+        _lib.check(L.ic_gdn_bwd(ax, _lib.ptr(norm), _lib.ptr(gy), _lib.ptr(g), ctx.inverse, adx, _lib.ptr(dg),
+                                _lib.ptr(dbeta), _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_bwd")
+        return dx, dg, dbeta, None
+
+
+def gdn(x, gamma, beta, inverse=False):
+    return GDNFn.apply(x, gamma, beta, bool(inverse))
+
+
+class NonNegFn(Function):
+    """NonNegativeParam.forward (gdn.py:59-62): max(p, bound)^2 - pedestal."""
+
+    @staticmethod
+    def forward(ctx, p, bound, pedestal):
+        _lib.require_device(p)
+        p = p.contiguous()
+        out = torch.empty_like(p)
+        _lib.check(_L().ic_nonneg_fwd(_lib.ptr(p), _n(p), float(bound), float(pedestal), _lib.ptr(out),
+                                      _lib.stream_of(p)), "nonneg_fwd")
+        ctx.bound = float(bound)
+        ctx.save_for_backward(p)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (p,) = ctx.saved_tensors
+        g = _match(g, p)
+        gi = torch.empty_like(p)
+        _lib.check(_L().ic_nonneg_bwd(_lib.ptr(p), _lib.ptr(g), _n(p), ctx.bound, _lib.ptr(gi),
+                                      _lib.stream_of(p)), "nonneg_bwd")
+        return gi, None, None
+
+
+# ============================================================== elementwise
+class BoundFn(Function):
+    @staticmethod
+    def forward(ctx, x, bound, upper):
+        _lib.require_device(x)
+        x = _dense(x)
+        y = torch.empty_like(x)
+        _lib.check(_L().ic_bound_fwd(_lib.ptr(x), _n(x), float(bound), int(upper), _lib.ptr(y),
+                                     _lib.stream_of(x)), "bound_fwd")
+        ctx.conf = (float(bound), int(upper))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        bound, upper = ctx.conf
+        g = _match(g, x)
+        gx = torch.empty_like(x)
+        _lib.check(_L().ic_bound_bwd(_lib.ptr(x), _lib.ptr(g), _n(x), bound, upper, _lib.ptr(gx),
+                                     _lib.stream_of(x)), "bound_bwd")
+        return gx, None, None
+
+
+class ReLUFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        _lib.require_device(x)
+        x = _dense(x)
+        y = torch.empty_like(x)
+        _lib.check(_L().ic_relu_fwd(_lib.ptr(x), _n(x), _lib.ptr(y), _lib.stream_of(x)), "relu_fwd")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        return relu_bwd(y, g)
+
+
+def relu_bwd(y, g):
+    g = _match(g, y)
+    gx = torch.empty_like(y)
+    _lib.check(_L().ic_relu_bwd(_lib.ptr(y), _lib.ptr(g), _n(y), _lib.ptr(gx), _lib.stream_of(y)), "relu_bwd")
+    return gx
+
+
+class AbsFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        _lib.require_device(x)
+        x = _dense(x)
+        y = torch.empty_like(x)
+        _lib.check(_L().ic_abs_fwd(_lib.ptr(x), _n(x), _lib.ptr(y), _lib.stream_of(x)), "abs_fwd")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        g = _match(g, x)
+        gx = torch.empty_like(x)
+        _lib.check(_L().ic_abs_bwd(_lib.ptr(x), _lib.ptr(g), _n(x), _lib.ptr(gx), _lib.stream_of(x)), "abs_bwd")
+        return gx
+
+
+class ExpClampFn(Function):
+    """torch.clamp(v.exp(), lo, hi) of prior_synthesis.py:72."""
+
+    @staticmethod
+    def forward(ctx, v, lo, hi):
+        _lib.require_device(v)
+        v = _dense(v)
+        s = torch.empty_like(v)
+        e = torch.empty_like(v)
+        _lib.check(_L().ic_exp_clamp_fwd(_lib.ptr(v), _n(v), float(lo), float(hi), _lib.ptr(s), _lib.ptr(e),
+                                         _lib.stream_of(v)), "exp_clamp_fwd")
+        ctx.conf = (float(lo), float(hi))
+        ctx.save_for_backward(e)
+        return s
+
+    @staticmethod
+    def backward(ctx, g):
+        (e,) = ctx.saved_tensors
+        lo, hi = ctx.conf
+        g = _match(g, e)
+        gv = torch.empty_like(e)
+        _lib.check(_L().ic_exp_clamp_bwd(_lib.ptr(e), _lib.ptr(g), _n(e), lo, hi, _lib.ptr(gv),
+                                         _lib.stream_of(e)), "exp_clamp_bwd")
+        return gv, None, None
+
+
+# ============================================================== losses
+class CELossFn(Function):
+    """_ce_loss (entropy_model.py:185): sum clamp(-ln(p+1e-10)/ln 2, 0, 50)."""
+
+    @staticmethod
+    def forward(ctx, p):
+        _lib.require_device(p)
+        p = _dense(p)
+        out = torch.empty((), device=p.device, dtype=torch.float32)
+        L = _L()
+        nb = L.ic_reduce_ws(p.numel())
+        buf = _ws(nb, p.device)
+        _lib.check(L.ic_ce_loss_fwd(_lib.ptr(p), _n(p), _lib.ptr(out), _lib.ptr(buf), nb, _lib.stream_of(p)),
+                   "ce_loss_fwd")
+        ctx.save_for_backward(p)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (p,) = ctx.saved_tensors
+        g = g.contiguous()
+        gp = torch.empty_like(p)
+        _lib.check(_L().ic_ce_loss_bwd(_lib.ptr(p), _lib.ptr(g), _n(p), _lib.ptr(gp), _lib.stream_of(p)),
+                   "ce_loss_bwd")
+        return gp
+
+
+class MSEFn(Function):
+    """nn.MSELoss(reduction='mean')(input, target)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        _lib.require_device(a, b)
+        a = _dense(a)
+        b = _match(b, a)
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        L = _L()
+        nb = L.ic_reduce_ws(a.numel())
+        buf = _ws(nb, a.device)
+        _lib.check(L.ic_mse_fwd(_lib.ptr(a), _lib.ptr(b), _n(a), _lib.ptr(out), _lib.ptr(buf), nb,
+                                _lib.stream_of(a)), "mse_fwd")
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
+        _lib.check(_L().ic_mse_bwd(_lib.ptr(a), _lib.ptr(b), _lib.ptr(g), _n(a), _lib.ptr(ga), _lib.ptr(gb),
+                                   _lib.stream_of(a)), "mse_bwd")
+        return ga, gb
+
+
+# ============================================================== entropy models
+def _to_last(t):
+    """(N, C, *) -> dense (N, *, C) so that channel = flat index % C."""
+    return t.movedim(1, -1).contiguous()
+
+
+def _from_last(t):
+    return t.movedim(-1, 1)
+
+
+class FactorizedFn(Function):
+    """EntropyModel._quantize + _prob_mass (entropy_model.py:216-269).
+    Returns (q, p) in the input's logical (N, C, *) shape."""
+
+    @staticmethod
+    def forward(ctx, z, mode, u, seed, offset, *params):
+        _lib.require_device(z, u, *params)
+        L = _L()
+        C = z.shape[1]
+        zl = _to_last(z)
+        ul = None if u is None else _to_last(u.to(z.dtype))
+        q = torch.empty_like(zl)
+        p = torch.empty_like(zl)
+        prm = [t.contiguous() for t in params]
+        cp = _lib.ICFactParams(*[ctypes.c_void_p(t.data_ptr()) for t in prm])
+        _lib.check(L.ic_factorized_fwd(_lib.ptr(zl), _n(zl), C, ctypes.byref(cp), int(mode), _lib.ptr(ul),
+                                       ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset), _lib.ptr(q),
+                                       _lib.ptr(p), _lib.stream_of(z)), "factorized_fwd")
+        ctx.mode = int(mode)
+        ctx.C = C
+        ctx.save_for_backward(q, *prm)
+        return _from_last(q), _from_last(p)
+
+    @staticmethod
+    def backward(ctx, gq, gp):
+        q, *prm = ctx.saved_tensors
+        L = _L()
+        gql = None if gq is None else _to_last(gq)
+        gpl = None if gp is None else _to_last(gp)
+        dz = torch.empty_like(q)
+        grads = [torch.empty_like(t) for t in prm]
+        cp = _lib.ICFactParams(*[ctypes.c_void_p(t.data_ptr()) for t in prm])
+        cg = _lib.ICFactGrads(*[ctypes.c_void_p(t.data_ptr()) for t in grads])
+        _lib.check(L.ic_factorized_bwd(_lib.ptr(q), _n(q), ctx.C, ctypes.byref(cp),
+                                       None if ctx.mode == 1 else _lib.ptr(gql), _lib.ptr(gpl), _lib.ptr(dz),
+                                       ctypes.byref(cg), _lib.stream_of(q)), "factorized_bwd")
+        if ctx.mode == 1:  # torch.round has zero gradient
+            dz.zero_()
+        return (_from_last(dz), None, None, None, None, *grads)
+
+
+class ConditionalFn(Function):
+    """SymmetricConditionalModel._quantize + _prob_mass (entropy_model.py:319-352)."""
+
+    @staticmethod
+    def forward(ctx, y, scale, mean, kind, mode, u, seed, offset):
+        _lib.require_device(y, scale, mean, u)
+        L = _L()
+        y = _dense(y)
+        scale = _match(scale, y)
+        if mean is not None:
+            mean = _match(mean, y)
+        if u is not None:
+            u = _match(u.to(y.dtype), y)
+        q = torch.empty_like(y)
+        p = torch.empty_like(y)
+        _lib.check(L.ic_conditional_fwd(_lib.ptr(y), _lib.ptr(scale), _lib.ptr(mean), _n(y), int(kind), int(mode),
+                                        _lib.ptr(u), ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset),
+                                        _lib.ptr(q), _lib.ptr(p), _lib.stream_of(y)), "conditional_fwd")
+        ctx.conf = (int(kind), int(mode), mean is not None)
+        ctx.save_for_backward(q, scale, mean)
+        return q, p
+
+    @staticmethod
+    def backward(ctx, gq, gp):
+        q, scale, mean = ctx.saved_tensors
+        kind, mode, has_mean = ctx.conf
+        L = _L()
+        gq = None if gq is None else _match(gq, q)
+        gp = None if gp is None else _match(gp, q)
+        dy = torch.empty_like(q) if ctx.needs_input_grad[0] else None
+        ds = torch.empty_like(q) if ctx.needs_input_grad[1] else None
+        dm = torch.empty_like(q) if (has_mean and ctx.needs_input_grad[2]) else None
+        _lib.check(L.ic_conditional_bwd(_lib.ptr(q), _lib.ptr(scale), _lib.ptr(mean), _n(q), kind,
+                                        _lib.ptr(gq), _lib.ptr(gp), _lib.ptr(dy), _lib.ptr(ds), _lib.ptr(dm),
+                                        _lib.stream_of(q)), "conditional_bwd")
+        if mode == 1 and dy is not None:  # round: zero gradient through q
+            if gp is None:
+                dy.zero_()
+            else:
+                dy.zero_()
+        return dy, ds, dm, None, None, None, None, None
+
+
+def factorized(z, params, train, u=None):
+    """Returns (q, p) for EntropyModel; `u` optional injected U[0,1) draws."""
+    if not train:
+        mode, seed, off = 1, 0, 0
+    elif u is not None:
+        mode, seed, off = 0, 0, 0
+    else:
+        mode = 2
+        seed, off = _noise.philox_stream(z.numel())
+    return FactorizedFn.apply(z, mode, u, seed, off, *params)
+
+
+def conditional(y, scale, mean, kind, train, u=None):
+    if not train:
+        mode, seed, off = 1, 0, 0
+    elif u is not None:
+        mode, seed, off = 0, 0, 0
+    else:
+        mode = 2
+        seed, off = _noise.philox_stream(y.numel())
+    return ConditionalFn.apply(y, scale, mean, kind, mode, u, seed, off)
+
+
+class SqDiffFn(Function):
+    """(a - b)^2 elementwise: nn.MSELoss(reduction='none')."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        _lib.require_device(a, b)
+        a = _dense(a)
+        b = _match(b, a)
+        out = torch.empty_like(a)
+        _lib.check(_L().ic_sqdiff_fwd(_lib.ptr(a), _lib.ptr(b), _n(a), _lib.ptr(out), _lib.stream_of(a)),
+                   "sqdiff_fwd")
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = _match(g, a)
+        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
+        _lib.check(_L().ic_sqdiff_bwd(_lib.ptr(a), _lib.ptr(b), _lib.ptr(g), _n(a), _lib.ptr(ga), _lib.ptr(gb),
+                                      _lib.stream_of(a)), "sqdiff_bwd")
+        return ga, gb
+
+
+class MSSSIMFn(Function):
+    """SSIM / MS-SSIM loss (modelling/loss.py:48-188)."""
+
+    @staticmethod
+    def forward(ctx, a, b, conf):
+        _lib.require_device(a, b)
+        L = _L()
+        a = a.contiguous()
+        b = b.contiguous()
+        N, C, H, W = a.shape
+        (nlev, fs, sigma, max_val, log_scale, single, k1, k2, eps, weights) = conf
+        sb = L.ic_msssim_state_bytes(N, C, H, W, nlev, fs)
+        if sb == 0:
+            raise RuntimeError(f"ms-ssim: image {H}x{W} too small for {nlev} levels of a {fs}x{fs} window")
+        state = torch.empty(sb // 4, device=a.device, dtype=torch.float32)
+        nb = L.ic_msssim_ws(N, C, H, W, nlev, fs)
+        buf = _ws(nb, a.device)
+        wts = (ctypes.c_float * nlev)(*weights)
+        out = torch.empty((N,) if (single and log_scale) else (), device=a.device, dtype=torch.float32)
+        _lib.check(L.ic_msssim_fwd(_lib.ptr(a), _lib.ptr(b), N, C, H, W, nlev, fs, sigma, max_val, int(log_scale),
+                                   int(single), k1, k2, eps, ctypes.cast(wts, ctypes.c_void_p), _lib.ptr(out),
+                                   _lib.ptr(state), _lib.ptr(buf), nb, _lib.stream_of(a)), "msssim_fwd")
+        ctx.conf = conf
+        ctx.shape = (N, C, H, W)
+        ctx.save_for_backward(state)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (state,) = ctx.saved_tensors
+        L = _L()
+        N, C, H, W = ctx.shape
+        (nlev, fs, sigma, max_val, log_scale, single, k1, k2, eps, weights) = ctx.conf
+        g = g.contiguous()
+        ga = torch.empty((N, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        gb = torch.empty((N, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        nb = L.ic_msssim_ws(N, C, H, W, nlev, fs)
+        buf = _ws(nb, g.device)
+        wts = (ctypes.c_float * nlev)(*weights)
+        _lib.check(L.ic_msssim_bwd(N, C, H, W, nlev, fs, sigma, max_val, int(log_scale), int(single), k1, k2, eps,
+                                   ctypes.cast(wts, ctypes.c_void_p), _lib.ptr(g), _lib.ptr(state), _lib.ptr(ga),
+                                   _lib.ptr(gb), _lib.ptr(buf), nb, _lib.stream_of(g)), "msssim_bwd")
+        return ga, gb, None
+
+
+def msssim(img1, img2, mod, weights, single_scale):
+    conf = (len(weights), int(mod.filter_size), float(mod.filter_sigma), float(mod.max_val), bool(mod.log_scale),
+            bool(single_scale), float(mod.k1), float(mod.k2), float(mod.eps), [float(w) for w in weights])
+    return MSSSIMFn.apply(img1, img2, conf)

@@ -1,0 +1,43 @@
+"""GDN / IGDN / RGDN (reference modelling/layers/gdn.py:42-88) on HIP.
+
+y = x / sqrt(beta + conv1x1(x^2, gamma))   (inverse: x * sqrt(...); relu: ReLU first)
+gamma, beta are re-parameterised by NonNegativeParam: max(p, bound)^2 - pedestal.
+The 1x1 "conv" is a CxC GEMM on fp32 MFMA with x^2 formed in the operand load
+and the divide fused in the epilogue (csrc/gdn.hip)."""
+import torch
+import torch.nn as nn
+
+from ...functional import GDNFn, NonNegFn, ReLUFn
+
+
+class NonNegativeParam(nn.Module):
+    """reference gdn.py:42-62.  `pedestal`/`bound` are plain attributes (not
+    buffers), so the state dict holds only `param`, as in the reference."""
+
+    def __init__(self, init_val, minimum=0, offset=2 ** (-18)):
+        super().__init__()
+        ped = torch.tensor(float(offset) ** 2)           # fp32, like the reference
+        self.pedestal = ped
+        self.bound = (float(minimum) + ped.clone().detach() ** 2) ** 0.5
+        self.param = nn.Parameter(torch.sqrt(torch.max(init_val + ped, ped)))
+
+    def forward(self):
+        return NonNegFn.apply(self.param, float(self.bound), float(self.pedestal))
+
+
+class GDN(nn.Module):
+    def __init__(self, in_channels, inverse=False, relu=False,
+                 gamma_init=0.1, beta_min=1e-6, offset=2 ** -18):
+        super().__init__()
+        self.inverse = inverse
+        self.relu = relu
+        # the reference builds both parameters with NonNegativeParam's default
+        # offset (its `offset` argument is accepted but unused, gdn.py:69-74)
+        eye = torch.eye(in_channels).view(in_channels, in_channels, 1, 1)
+        self.gamma = NonNegativeParam(eye * gamma_init)
+        self.beta = NonNegativeParam(torch.ones((in_channels,)), minimum=beta_min)
+
+    def forward(self, x):
+        if self.relu:
+            x = ReLUFn.apply(x)
+        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse))

@@ -1,0 +1,67 @@
+"""Compressor2018 — Balle et al. 2018 scale hyperprior (reference
+modelling/meta_arch/bmshl2018.py:49-110), every tensor op on HIP kernels.
+
+forward(x) -> (x_tilde.detach(), losses) with losses =
+{z_entropy, y_entropy, bpp, total_loss, <distortion names>}; only
+total_loss carries grad."""
+import torch.nn as nn
+
+from ...functional import AbsFn
+from ..blocks import (ENTROPY_MODEL_REGISTRY, AnalysisTransform, HyperpriorAnalysisTransform,
+                      HyperpriorSynthesisTransform, SynthesisTransform)
+from ..layers import LowerBound, UpperBound
+from ..loss import get_loss_dict
+from .build import META_ARCH_REGISTRY
+
+
+@META_ARCH_REGISTRY.register()
+class Compressor2018(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.analysis_transform = AnalysisTransform(cfg)
+        self.prior_analysis = HyperpriorAnalysisTransform(cfg)
+        self.prior_synthesis = HyperpriorSynthesisTransform(cfg)
+        self.synthesis_transform = SynthesisTransform(cfg)
+        # The reference sizes the factorized model with LATENT_CHANNELS while z
+        # carries INTER_CHANNELS (crash when they differ); z's
+        # channel count is used here, identical whenever the reference runs.
+        self.entropy_model = ENTROPY_MODEL_REGISTRY.get("EntropyModel")(cfg.MODEL.INTER_CHANNELS, cfg)
+        self.conditional_model = ENTROPY_MODEL_REGISTRY.get(cfg.MODEL.ENTROPY_MODEL.CONDITIONAL_MODEL)(cfg)
+        self.distortion_loss_fns = get_loss_dict(cfg, cfg.MODEL.LOSS.DISTORTION_LOSS_NAMES)
+        self.distortion_loss_weight = cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT
+        self.loss_names = ["y_entropy", "z_entropy", "bpp"] + list(self.distortion_loss_fns.keys())
+
+    def forward(self, x):
+        N, _, H, W = x.shape
+        num_pixels = N * H * W
+        y = self.analysis_transform(x)
+        z = self.prior_analysis(AbsFn.apply(y))
+        z_tilde, _z_probs, z_ce = self.entropy_model(z)
+        sigma = self.prior_synthesis(z_tilde)
+        y_tilde, y_probs = self.conditional_model(y, sigma)
+        y_ce = self.conditional_model._ce_loss(y_probs)
+        x_tilde = self.synthesis_transform(y_tilde)
+        x_tilde = LowerBound.apply(UpperBound.apply(x_tilde, 1.), 0.)
+
+        dist = self.distortion_loss(x, x_tilde)
+        total_dist = sum(dist.values())
+        entropy = (z_ce + y_ce) / num_pixels
+        total = self.distortion_loss_weight * total_dist + entropy
+        losses = {
+            "z_entropy": z_ce.detach() / num_pixels,
+            "y_entropy": y_ce.detach() / num_pixels,
+            "bpp": entropy.detach(),
+            "total_loss": total,
+        }
+        losses.update({k: v.detach() for k, v in dist.items()})
+        return x_tilde.detach(), losses
+
+    def distortion_loss(self, img1, img2):
+        return {name: fn(img1, img2) for name, fn in self.distortion_loss_fns.items()}
+
+    def compress(self, x):
+        """Stub in the reference (bmshl2018.py:106-107): no entropy coder."""
+        return None
+
+    def decompress(self, x):
+        return None

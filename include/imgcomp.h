@@ -1,0 +1,183 @@
+/*
+ * imgcomp.h — C ABI of libimgcomp.so, the MI355X (gfx950) kernels behind the
+ * Balle-2018 scale-hyperprior hot path of hieu1999210/image_compression.
+ *
+ * Every entry point:
+ *   - takes raw device pointers (fp32), plain sizes and a hipStream_t
+ *     (passed as void* so this header needs no HIP include);
+ *   - launches asynchronously on that stream; never allocates, frees or
+ *     synchronises (graph-capturable); keeps no pointer after it returns;
+ *   - returns 0 on success, a hipError_t value on a launch failure, or
+ *     IC_ERR_ARG (1001) / IC_ERR_WORKSPACE (1002).  The Python host layer
+ *     turns any non-zero status into RuntimeError (reference error
+ *     behaviour: torch raises RuntimeError on bad shapes).
+ *   - Ops that need scratch take (ws, ws_bytes); the matching *_ws() query
+ *     returns the byte count for the same arguments.
+ *
+ * Activations are described by ic_act: logical [n][c][h][w] with arbitrary
+ * element strides.  The GEMM fast paths want channel stride 1 (NHWC,
+ * torch.channels_last); other layouts take the generic gather path.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   conv2d_*            torch.nn.Conv2d in modelling/blocks/analysis.py:55,
+ *                       modelling/blocks/prior_analysis.py:54-56
+ *   conv_transpose2d_*  torch.nn.ConvTranspose2d in modelling/blocks/synthesis.py:55-57,
+ *                       modelling/blocks/prior_synthesis.py:54-56
+ *   gdn_*               modelling/layers/gdn.py:79-88 (GDN.forward)
+ *   nonneg_*            modelling/layers/gdn.py:59-62 (NonNegativeParam.forward)
+ *   bound_*             modelling/layers/bound.py:28-59 (LowerBound / UpperBound)
+ *   relu_*, abs_*       nn.ReLU (prior_*.py), torch.abs (meta_arch/bmshl2018.py:72)
+ *   exp_clamp_*         modelling/blocks/prior_synthesis.py:72
+ *   factorized_*        modelling/blocks/entropy_model.py:204-269 (EntropyModel)
+ *   conditional_*       modelling/blocks/entropy_model.py:280-378 (Laplacian/Gaussian)
+ *   ce_loss_*           modelling/blocks/entropy_model.py:171-185 (_ce_loss)
+ *   mse_*, sqdiff_*     nn.MSELoss(reduction="mean"/"none") in modelling/loss.py:25
+ *   msssim_*            modelling/loss.py:48-188 (SSIMLoss, MS_SSIMLoss)
+ */
+#ifndef IMGCOMP_H
+#define IMGCOMP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IC_ERR_ARG 1001
+#define IC_ERR_WORKSPACE 1002
+
+typedef struct ic_act {
+  float* data;
+  int n, c, h, w;
+  long long sn, sc, sh, sw; /* element strides */
+} ic_act;
+
+/* ---- library ---- */
+int ic_version(void);                 /* ABI version (monotonic) */
+int ic_device_sync_check(void* stream); /* hipStreamQuery-free no-op launch test */
+
+/* ---- Conv2d (k x k, stride, zero pad): y = conv(x, w) + b, act 0=none 1=relu
+ *      w: [Cout][Cin][k][k]; b: [Cout] or NULL; y->c = Cout, y->h = (x->h+2pad-k)/stride+1 */
+size_t ic_conv2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y);
+int ic_conv2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                  const ic_act* y, int act, void* ws, size_t ws_bytes, void* stream);
+/* dx = conv2d input-gradient of dy (no bias); dx->c = Cin */
+size_t ic_conv2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx);
+int ic_conv2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx,
+                    void* ws, size_t ws_bytes, void* stream);
+/* dw [Cout][Cin][k][k] = weight gradient; db [Cout] (optional, NULL to skip) */
+size_t ic_conv2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad);
+int ic_conv2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw,
+                    float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- ConvTranspose2d: w [Cin][Cout][k][k]; y->h = (x->h-1)*stride - 2pad + k + output_padding */
+size_t ic_conv_transpose2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y);
+int ic_conv_transpose2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride,
+                            int pad, const ic_act* y, int act, void* ws, size_t ws_bytes,
+                            void* stream);
+size_t ic_conv_transpose2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx);
+int ic_conv_transpose2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad,
+                              const ic_act* dx, void* ws, size_t ws_bytes, void* stream);
+size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad);
+int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad,
+                              float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- GDN: norm = beta + conv1x1(x^2, gamma); y = x / sqrt(norm) (inverse: x * sqrt(norm)).
+ *      gamma [C][C], beta [C] (already re-parameterised); x, y, norm share one layout. */
+size_t ic_gdn_fwd_ws(const ic_act* x);
+int ic_gdn_fwd(const ic_act* x, const float* gamma, const float* beta, int inverse,
+               const ic_act* y, float* norm, void* ws, size_t ws_bytes, void* stream);
+size_t ic_gdn_bwd_ws(const ic_act* x);
+int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+               const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+               void* stream);
+
+/* ---- elementwise on dense storage of n elements ---- */
+/* NonNegativeParam: v = max(p, bound); out = v*v - ped */
+int ic_nonneg_fwd(const float* p, long long n, float bound, float ped, float* out, void* stream);
+int ic_nonneg_bwd(const float* p, const float* gout, long long n, float bound, float* gin, void* stream);
+/* LowerBound (upper=0): max(x,b); UpperBound (upper=1): min(x,b) — with the reference's
+ * pass-through gradients */
+int ic_bound_fwd(const float* x, long long n, float bound, int upper, float* y, void* stream);
+int ic_bound_bwd(const float* x, const float* g, long long n, float bound, int upper, float* gx,
+                 void* stream);
+int ic_relu_fwd(const float* x, long long n, float* y, void* stream);
+int ic_relu_bwd(const float* y, const float* g, long long n, float* gx, void* stream);
+int ic_abs_fwd(const float* x, long long n, float* y, void* stream);
+int ic_abs_bwd(const float* x, const float* g, long long n, float* gx, void* stream);
+/* sigma = clamp(exp(v), lo, hi); saves e = exp(v) for the backward */
+int ic_exp_clamp_fwd(const float* v, long long n, float lo, float hi, float* sigma, float* e,
+                     void* stream);
+int ic_exp_clamp_bwd(const float* e, const float* g, long long n, float lo, float hi, float* gv,
+                     void* stream);
+
+/* ---- reductions (deterministic, two-level) ---- */
+size_t ic_reduce_ws(long long n);
+/* out[0] = sum clamp(-ln(p+1e-10)/ln2, 0, 50) */
+int ic_ce_loss_fwd(const float* p, long long n, float* out, void* ws, size_t ws_bytes, void* stream);
+/* gp = gout[0] * d/dp (gout: device scalar) */
+int ic_ce_loss_bwd(const float* p, const float* gout, long long n, float* gp, void* stream);
+/* out[0] = mean((a-b)^2) */
+int ic_mse_fwd(const float* a, const float* b, long long n, float* out, void* ws, size_t ws_bytes,
+               void* stream);
+/* ga = gout*2(a-b)/n (NULL to skip), gb = -ga (NULL to skip) */
+int ic_mse_bwd(const float* a, const float* b, const float* gout, long long n, float* ga, float* gb,
+               void* stream);
+
+/* ---- noise: u[i] = Philox4x32-10(seed, offset + i) -> U[0,1) ---- */
+int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset,
+               void* stream);
+
+/* ---- factorized entropy model (z): C channels, elements e with channel c = idx % C
+ *      (channels-last storage). params (device, fp32, reference shapes flattened):
+ *      w0[C*3] b0[C*3] f0[C*3] w1[C*9] b1[C*3] f1[C*3] w2[C*9] b2[C*3] f2[C*3] w3[C*3] b3[C]
+ *      mode: 0 = noise with given u (u in [0,1), y = z + (u - 0.5)), 1 = round,
+ *            2 = noise from Philox(seed, offset) */
+typedef struct ic_fact_params {
+  const float *w0, *b0, *f0, *w1, *b1, *f1, *w2, *b2, *f2, *w3, *b3;
+} ic_fact_params;
+int ic_factorized_fwd(const float* z, long long n, int C, const ic_fact_params* prm, int mode,
+                      const float* u, unsigned long long seed, unsigned long long offset,
+                      float* q, float* p, void* stream);
+/* given dq (NULL = 0) and dp (NULL = 0): dz (= dq + through p) and per-channel
+ * parameter gradients (same layout as params; written, not accumulated) */
+typedef struct ic_fact_grads {
+  float *w0, *b0, *f0, *w1, *b1, *f1, *w2, *b2, *f2, *w3, *b3;
+} ic_fact_grads;
+int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* prm,
+                      const float* dq, const float* dp, float* dz, const ic_fact_grads* grd,
+                      void* stream);
+
+/* ---- conditional (Laplacian kind=0 / Gaussian kind=1), mean = 0 or tensor ----
+ *      q = y + (u - 0.5) (mode 0), round(y) (mode 1), Philox (mode 2)
+ *      p = F((0.5-|q-mean|)/scale) - F((-0.5-|q-mean|)/scale) */
+int ic_conditional_fwd(const float* y, const float* scale, const float* mean, long long n, int kind,
+                       int mode, const float* u, unsigned long long seed,
+                       unsigned long long offset, float* q, float* p, void* stream);
+int ic_conditional_bwd(const float* q, const float* scale, const float* mean, long long n, int kind,
+                       const float* dq, const float* dp, float* dy, float* dscale, float* dmean,
+                       void* stream);
+
+/* ---- SSIM / MS-SSIM (modelling/loss.py:48-188) on [N][C][H][W] contiguous images in [0,1].
+ *      nlev levels (MS-SSIM: 5, weights[nlev] host array; single=1 for SSIMLoss, nlev=1).
+ *      out: log_scale && single -> out[N] = -log(max(ssim_n, eps)); else out[0] = loss.
+ *      `state` (ic_msssim_state_bytes) is written by fwd and read by bwd. */
+size_t ic_msssim_state_bytes(int N, int C, int H, int W, int nlev, int filter_size);
+size_t ic_msssim_ws(int N, int C, int H, int W, int nlev, int filter_size);
+int ic_msssim_fwd(const float* a, const float* b, int N, int C, int H, int W, int nlev, int filter_size,
+                  float filter_sigma, float max_val, int log_scale, int single, float k1, float k2,
+                  float eps, const float* weights, float* out, float* state, void* ws, size_t ws_bytes,
+                  void* stream);
+int ic_msssim_bwd(int N, int C, int H, int W, int nlev, int filter_size, float filter_sigma,
+                  float max_val, int log_scale, int single, float k1, float k2, float eps,
+                  const float* weights, const float* gout, const float* state, float* ga, float* gb,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* ---- elementwise squared difference (MSE with reduction="none") ---- */
+int ic_sqdiff_fwd(const float* a, const float* b, long long n, float* out, void* stream);
+int ic_sqdiff_bwd(const float* a, const float* b, const float* g, long long n, float* ga, float* gb,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,53 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) against golden vectors produced by the
+real reference (tools/gen_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import (assert_close, golden_names, load_golden, oracle_kwargs,
+                      params_of, rel_err)
+from oracle import ref_cpu
+
+SMALL = golden_names("small_")
+
+
+@pytest.mark.parametrize("name", SMALL)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_oracle_matches_reference(name, dtype):
+    meta, d = load_golden(name)
+    train = meta["train"]
+    out, losses, grads = ref_cpu.run(
+        params_of(d), d["x"], d["u_z"] if train else None,
+        d["u_y"] if train else None, train=train, dtype=dtype, **oracle_kwargs(meta))
+    tol = 2e-5 if dtype == torch.float32 else 1e-4
+    for k in ["y", "z", "z_tilde", "p_z", "sigma", "y_tilde", "p_y", "x_tilde_raw", "x_tilde"]:
+        ref = d["out/" + k]
+        got = out[k].detach().numpy()
+        if not train and k in ("z_tilde", "y_tilde", "p_z", "p_y", "sigma", "x_tilde_raw", "x_tilde"):
+            # eval mode rounds: an fp64 pre-round value within ~1e-6 of a .5
+            # boundary may round the other way; require near-total agreement.
+            if dtype == torch.float64:
+                assert rel_err(got, ref) < 5e-3, k
+                continue
+        assert_close(got, ref, tol, name=f"{name}:{k}")
+    for k in meta["loss_names"] + ["total_loss"]:
+        assert_close(losses[k].detach().numpy(), d["loss/" + k], tol, name=f"{name}:loss:{k}")
+    for k, g in grads.items():
+        ref = d["grad/" + k]
+        assert rel_err(g.numpy(), ref) < (5e-5 if dtype == torch.float32 else 5e-4), (name, k, rel_err(g.numpy(), ref))
+
+
+def test_gdn_known_answers():
+    """The reference's own known-answer tests (test/test_gdn.py:20-48):
+    at init GDN(x) = x / sqrt(1 + 0.1 x^2), IGDN = x * sqrt(...), RGDN = GDN(relu(x))."""
+    torch.manual_seed(0)
+    gp, bp = ref_cpu.gdn_init(3)
+    x = torch.rand(2, 3, 4, 5)
+    exp = x / torch.sqrt(1 + 0.1 * x ** 2)
+    assert (ref_cpu.gdn(x, gp, bp) - exp).abs().max() <= 1e-6
+    exp = x * torch.sqrt(1 + 0.1 * x ** 2)
+    assert (ref_cpu.gdn(x, gp, bp, inverse=True) - exp).abs().max() <= 1e-6
+    x = torch.rand(2, 3, 4, 5) - 0.5
+    xr = torch.clamp(x, min=0)
+    exp = xr / torch.sqrt(1 + 0.1 * xr ** 2)
+    assert (ref_cpu.gdn(x, gp, bp, relu=True) - exp).abs().max() <= 1e-6
