@@ -30,6 +30,94 @@ void set_y(IgDesc& d, const ic_act* y) {
   d.y = y->data; d.ys_n = y->sn; d.ys_h = y->sh; d.ys_w = y->sw; d.ys_c = y->sc; d.Cout = y->c;
 }
 
+
+constexpr int FEW_CH = 8;  // image-edge layers (3 channels) go through im2col / col2im
+
+// few input channels: xcol = im2col(x) (K = k*k*C padded to 32), then one 1x1 GEMM
+int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
+                  const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  const int T = k * k;
+  const int Kp = (int)ic_align((size_t)T * x->c, 32);
+  const long long rows = (long long)x->n * y->h * y->w;
+  ic_act xc;
+  xc.data = nullptr; xc.n = x->n; xc.c = Kp; xc.h = y->h; xc.w = y->w;
+  xc.sn = (long long)y->h * y->w * Kp; xc.sc = 1; xc.sh = (long long)y->w * Kp; xc.sw = Kp;
+  IgDesc d = {};
+  set_x(d, &xc);
+  set_y(d, y);
+  d.stride = 1; d.generic = 0; d.bias = bias; d.epi = epi; d.a_op = AOP_NONE;
+  d.nphase = 1;
+  IgPhase& P = d.ph[0];
+  P.T = 1; P.dy[0] = 0; P.dx[0] = 0;
+  P.Hg = y->h; P.Wg = y->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;
+  d.Kc = Kp;
+  const size_t part = ig_plan(d);
+  const size_t xcb = (size_t)rows * Kp * 4;
+  const size_t wpb = (size_t)d.Npad * Kp * 4;
+  const size_t tot = ic_align(xcb, 256) + ic_align(wpb, 256) + ic_align(part, 256);
+  if (need) { *need = tot; return IC_OK; }
+  if (wsb < tot) return IC_ERR_WORKSPACE;
+  Carve cv{(char*)ws, 0};
+  float* xcol = cv.take(xcb);
+  float* wp = cv.take(wpb);
+  d.partial = part ? cv.take(part) : nullptr;
+  d.x = xcol;
+  P.wp = wp;
+  int ky[IC_MAXT], kx[IC_MAXT];
+  for (int t = 0; t < T; ++t) { ky[t] = t / k; kx[t] = t % k; }
+  int rc = im2col_run(x->data, x->sn, x->sc, x->sh, x->sw, x->n, x->c, x->h, x->w, y->h, y->w, stride, k, pad,
+                      Kp, xcol, s);
+  if (rc) return rc;
+  rc = pack_weights(W, y->c, x->c, k, 0, 1, T, ky, kx, d.Npad, Kp, wp, s);
+  if (rc) return rc;
+  return ig_run(d, s);
+}
+
+// few output channels of a transposed conv: ycol[p][(t,b)] = x[p] . W[:, b, t] (one 1x1 GEMM
+// with N = k*k*B) then the deterministic sub-pixel gather col2im (+bias, act)
+int transposed_col2im(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
+                      const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  if (epi != EPI_NONE && epi != EPI_RELU) return IC_ERR_ARG;
+  const int T = k * k;
+  const int ncol = T * y->c;
+  const long long rows = (long long)x->n * x->h * x->w;
+  ic_act yc;
+  yc.data = nullptr; yc.n = x->n; yc.c = ncol; yc.h = x->h; yc.w = x->w;
+  yc.sn = (long long)x->h * x->w * ncol; yc.sc = 1; yc.sh = (long long)x->w * ncol; yc.sw = ncol;
+  IgDesc d = {};
+  set_x(d, x);
+  set_y(d, &yc);
+  d.stride = 1;
+  d.generic = (x->c % 32 != 0) || (x->sc != 1);
+  d.bias = nullptr; d.epi = EPI_NONE; d.a_op = AOP_NONE;
+  d.nphase = 1;
+  IgPhase& P = d.ph[0];
+  P.T = 1; P.dy[0] = 0; P.dx[0] = 0;
+  P.Hg = x->h; P.Wg = x->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;
+  d.Kc = d.generic ? (int)ic_align((size_t)x->c, 32) : x->c;
+  const size_t part = ig_plan(d);
+  const size_t ycb = (size_t)rows * ncol * 4;
+  const size_t wpb = (size_t)d.Npad * d.Kc * 4;
+  const size_t tot = ic_align(ycb, 256) + ic_align(wpb, 256) + ic_align(part, 256);
+  if (need) { *need = tot; return IC_OK; }
+  if (wsb < tot) return IC_ERR_WORKSPACE;
+  Carve cv{(char*)ws, 0};
+  float* ycol = cv.take(ycb);
+  float* wp = cv.take(wpb);
+  d.partial = part ? cv.take(part) : nullptr;
+  d.y = ycol;
+  P.wp = wp;
+  int ky[IC_MAXT], kx[IC_MAXT];
+  for (int t = 0; t < T; ++t) { ky[t] = t / k; kx[t] = t % k; }
+  if (d.generic) return IC_ERR_ARG;  // A (input channels) is wide on every caller
+  int rc = pack_weights(W, x->c, y->c, k, 2, 0, T, ky, kx, d.Npad, d.Kc, wp, s);
+  if (rc) return rc;
+  rc = ig_run(d, s);
+  if (rc) return rc;
+  return col2im_run(ycol, ncol, x->n, x->h, x->w, bias, y->data, y->sn, y->sc, y->sh, y->sw, y->c, y->h, y->w, k,
+                    stride, pad, epi == EPI_RELU, s);
+}
+
 // y[a] = sum_{t,b} x[b] @ (gy*s + ky - pad) * W[a][b][ky][kx]   (W: [A=y->c][B=x->c][k][k])
 int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
                 const ic_act* y, int epi, int aop, const float* aux0, const float* aux1,
@@ -38,6 +126,8 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   if (x->n != y->n) return IC_ERR_ARG;
   if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w)
     return IC_ERR_ARG;
+  if (x->c <= FEW_CH && aop == AOP_NONE)
+    return direct_im2col(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need);
   IgDesc d = {};
   set_x(d, x);
   set_y(d, y);
@@ -76,6 +166,8 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if (x->n != y->n) return IC_ERR_ARG;
   if ((y->h + 2 * pad - k) / stride + 1 != x->h || (y->w + 2 * pad - k) / stride + 1 != x->w)
     return IC_ERR_ARG;
+  if (y->c <= FEW_CH && x->c % 32 == 0 && x->sc == 1)
+    return transposed_col2im(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need);
   IgDesc d = {};
   set_x(d, x);
   set_y(d, y);
@@ -148,17 +240,42 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   for (int t = 0; t < d.T; ++t) {
     d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
   }
+  // few X channels: wgrad against xcol = im2col(X) on G's grid (1 tap, K = Kp)
+  const bool few = X->c <= FEW_CH;
+  const int Kp = (int)ic_align((size_t)d.T * X->c, 32);
+  size_t xcb = 0;
+  if (few) {
+    xcb = (size_t)G->n * G->h * G->w * Kp * 4;
+    d.Hx = G->h; d.Wx = G->w; d.Cx = Kp; d.stride = 1; d.T = 1; d.dy[0] = 0; d.dx[0] = 0;
+    d.xs_c = 1; d.xs_w = Kp; d.xs_h = (long long)G->w * Kp; d.xs_n = (long long)G->h * G->w * Kp;
+    d.generic = 0;
+  }
   const size_t part = wg_plan(d);
   const size_t cs = db ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
-  const size_t tot = ic_align(part, 256) + ic_align(cs, 256);
+  const size_t tot = ic_align(part, 256) + ic_align(cs, 256) + ic_align(xcb, 256);
   if (need) { *need = tot; return IC_OK; }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   d.partial = cv.take(part);
   float* csw = cs ? cv.take(cs) : nullptr;
-  int rc = wg_run(d, s);
+  int rc;
+  if (few) {
+    float* xcol = cv.take(xcb);
+    d.x = xcol;
+    rc = im2col_run(X->data, X->sn, X->sc, X->sh, X->sw, X->n, X->c, X->h, X->w, G->h, G->w, stride, k, pad, Kp,
+                    xcol, s);
+    if (rc) return rc;
+  }
+  rc = wg_run(d, s);
   if (rc) return rc;
-  rc = wg_reduce(d, dw, kk_of_t, k * k, s);
+  if (few) {
+    // reduce the (t, c)-flattened columns straight into [g][c][ky][kx]
+    WgDesc r = d;
+    r.generic = 1; r.T = k * k; r.Cx = X->c;
+    rc = wg_reduce(r, dw, kk_of_t, k * k, s);
+  } else {
+    rc = wg_reduce(d, dw, kk_of_t, k * k, s);
+  }
   if (rc) return rc;
   if (db) {
     rc = colsum(bias_src->data, bias_src->sn, bias_src->sc, bias_src->sh, bias_src->sw, bias_src->n,

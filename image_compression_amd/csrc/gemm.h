@@ -96,6 +96,14 @@ int colsum(const float* t, long long s_n, long long s_c, long long s_h, long lon
 //  mode 0 (direct):     wp[t][a][b]   = W[a][b][ky_t][kx_t]   (out ch a, reduce b)
 //  mode 1 (transposed): wp[t][b][a]   = W[a][b][ky_t][kx_t]   (out ch b, reduce a)
 //  generic: the (t, reduce-ch) pair is flattened into a Kpad-long row.
+//  mode 2 (scatter):    wp[0][t*B + b][a] = W[a][b][ky_t][kx_t]   (rows n >= T*B zero)
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic,
                  int T, const int* ky, const int* kx, int Npad, int Kpad,
                  float* wp, hipStream_t s);
+
+// few-channel edges (im2col.hip)
+int im2col_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H,
+               int W, int Hg, int Wg, int stride, int k, int pad, int Kp, float* out, hipStream_t s);
+int col2im_run(const float* ycol, int ncol, int N, int Hi, int Wi, const float* bias, float* y, long long sn,
+               long long sc, long long sh, long long sw, int B, int Ho, int Wo, int k, int stride, int pad,
+               int act, hipStream_t s);

@@ -17,7 +17,8 @@ struct PackArgs {
 __global__ void pack_kernel(const PackArgs p) {
   const int Nout = p.mode == 0 ? p.A : p.B;
   const int R = p.mode == 0 ? p.B : p.A;
-  const long long total = p.generic ? (long long)p.Npad * p.Kpad : (long long)p.T * p.Npad * R;
+  const long long total = p.mode == 2 ? (long long)p.Npad * p.A
+                        : (p.generic ? (long long)p.Npad * p.Kpad : (long long)p.T * p.Npad * R);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     int t, n, r;
@@ -33,6 +34,15 @@ __global__ void pack_kernel(const PackArgs p) {
       t = (int)(tn / p.Npad);
     }
     float v = 0.f;
+    if (p.mode == 2) {
+      // i = n * A + a with n = tt * B + b
+      const int a = (int)(i % p.A);
+      const int nn = (int)(i / p.A);
+      const int tt = nn / p.B, b = nn - (nn / p.B) * p.B;
+      if (tt < p.T) v = p.W[(((long long)a * p.B + b) * p.k + p.ky[tt]) * p.k + p.kx[tt]];
+      p.wp[i] = v;
+      continue;
+    }
     if (n < Nout && t < p.T) {
       const int a = p.mode == 0 ? n : r;
       const int b = p.mode == 0 ? r : n;
@@ -51,7 +61,7 @@ int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int
   p.Npad = Npad; p.Kpad = Kpad;
   for (int t = 0; t < T; ++t) { p.ky[t] = ky[t]; p.kx[t] = kx[t]; }
   const int R = mode == 0 ? B : A;
-  const long long total = generic ? (long long)Npad * Kpad : (long long)T * Npad * R;
+  const long long total = mode == 2 ? (long long)Npad * A : (generic ? (long long)Npad * Kpad : (long long)T * Npad * R);
   long long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);

@@ -177,27 +177,56 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
 
 struct WgRed {
   const float* partial;
-  float* out;
-  int nsplit, Tp, T, Cg, Cx, ncols, kk, generic;
+  float* out;    // final [g][c][kk] (G == 1) or level-2 partial [G][g][t][c]
+  int nsplit, Tp, T, Cg, Cx, ncols, kk, generic, spg, G;
   int kk_of_t[IC_MAXT];
 };
 
+// thread = one (g, t, c) element and one group of `spg` splits; 4 independent
+// accumulators over the group (fixed order -> deterministic)
 __global__ void wg_reduce_kernel(const WgRed r) {
   const long long total = (long long)r.Cg * r.Cx * r.T;
+  const int grp = blockIdx.y;
+  const int s0 = grp * r.spg;
+  const int s1 = min(r.nsplit, s0 + r.spg);
+  const long long sstride = (long long)r.Tp * r.Cg * r.ncols;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    // i enumerates (g, t, c) with c fastest: coalesced slab reads
     const int c = (int)(i % r.Cx);
     const long long gt = i / r.Cx;
     const int t = (int)(gt % r.T);
     const int g = (int)(gt / r.T);
     const int tp = r.generic ? 0 : t;
     const int col = r.generic ? t * r.Cx + c : c;
-    const long long stride = (long long)r.Tp * r.Cg * r.ncols;
     const float* src = r.partial + ((long long)tp * r.Cg + g) * r.ncols + col;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int sp = s0;
+    for (; sp + 3 < s1; sp += 4) {
+      a0 += src[(long long)sp * sstride];
+      a1 += src[(long long)(sp + 1) * sstride];
+      a2 += src[(long long)(sp + 2) * sstride];
+      a3 += src[(long long)(sp + 3) * sstride];
+    }
+    for (; sp < s1; ++sp) a0 += src[(long long)sp * sstride];
+    const float v = (a0 + a1) + (a2 + a3);
+    if (r.G == 1)
+      r.out[((long long)g * r.Cx + c) * r.kk + r.kk_of_t[t]] = v;
+    else
+      r.out[(long long)grp * total + i] = v;
+  }
+}
+
+__global__ void wg_reduce2_kernel(const float* p2, int G, long long total, int Cx, int T, int kk,
+                                  const WgRed r, float* out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
     float v = 0.f;
-    for (int s = 0; s < r.nsplit; ++s) v += src[s * stride];
-    r.out[((long long)g * r.Cx + c) * r.kk + r.kk_of_t[t]] = v;
+    for (int q = 0; q < G; ++q) v += p2[(long long)q * total + i];
+    const int c = (int)(i % Cx);
+    const long long gt = i / Cx;
+    const int t = (int)(gt % T);
+    const int g = (int)(gt / T);
+    out[((long long)g * Cx + c) * kk + r.kk_of_t[t]] = v;
   }
 }
 
@@ -211,6 +240,7 @@ int wg_launch_t(const WgDesc& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- colsum
+// Generic strided form (small / non-NHWC tensors).
 __global__ void colsum_partial_kernel(const float* t, long long s_n, long long s_c, long long s_h,
                                       long long s_w, int N, int C, int H, int W, long long rows,
                                       long long rpb, float* part) {
@@ -229,22 +259,59 @@ __global__ void colsum_partial_kernel(const float* t, long long s_n, long long s
   }
 }
 
+// NHWC-dense form: rows x C, float4 per thread, rows interleaved over the
+// block's thread groups, then a fixed-order LDS combine per column.
+__global__ void __launch_bounds__(256) colsum_rows_kernel(const float* t, long long rows, int C, long long rpb,
+                                                          float* part) {
+  __shared__ float lds[8192];
+  const int c4n = C >> 2;            // float4 per row
+  const int groups = 256 / c4n;      // row groups
+  const int tid = threadIdx.x;
+  const int g = tid / c4n, c4 = tid - (tid / c4n) * c4n;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  long long r1 = r0 + rpb;
+  if (r1 > rows) r1 = rows;
+  floatx4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (g < groups) {
+    const float* base = t + (size_t)c4 * 4;
+    long long r = r0 + g;
+    for (; r + groups < r1; r += 2 * groups) {
+      acc0 += *(const floatx4v*)(base + (size_t)r * C);
+      acc1 += *(const floatx4v*)(base + (size_t)(r + groups) * C);
+    }
+    if (r < r1) acc0 += *(const floatx4v*)(base + (size_t)r * C);
+    acc0 += acc1;
+    *(floatx4v*)&lds[(g * c4n + c4) * 4] = acc0;
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float v = 0.f;
+    for (int q = 0; q < groups; ++q) v += lds[q * C + c];
+    part[(long long)blockIdx.x * C + c] = v;
+  }
+}
+
+// one wave per column: lanes stride over the block partials, fixed-order tree
 __global__ void colsum_final_kernel(const float* part, int nb, int C, float scale, float* out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   float acc = 0.f;
-  for (int b = 0; b < nb; ++b) acc += part[(long long)b * C + c];
-  out[c] = acc * scale;
+  for (int b = lane; b < nb; b += 64) acc += part[(long long)b * C + c];
+  acc = wave_sum(acc);
+  if (lane == 0) out[c] = acc * scale;
 }
 
 int colsum_blocks(long long rows) {
-  long long nb = (rows + 127) / 128;
-  if (nb > 1024) nb = 1024;
+  long long nb = (rows + 255) / 256;
+  if (nb > 512) nb = 512;
   if (nb < 1) nb = 1;
   return (int)nb;
 }
 
 }  // namespace
+
+constexpr int WG_SPG = 32;  // splits summed per thread in the first reduce level
 
 size_t wg_plan(WgDesc& d) {
   if (d.generic) { d.bm = 192; d.bn = 64; d.ncols = d.T * d.Cx; }
@@ -253,8 +320,9 @@ size_t wg_plan(WgDesc& d) {
   d.ntiles = ic_cdiv(d.ncols, d.bn);
   d.P = (long long)d.N * d.Hg * d.Wg;
   const long long tiles = (long long)d.mtiles * d.ntiles * (d.generic ? 1 : d.T);
-  long long ns = (1024 + tiles - 1) / tiles;
-  long long maxs = (d.P + 63) / 64;  // at least 64 pixels per split
+  // ~2 resident blocks per CU; never fewer than 64 pixels per split
+  long long ns = (512 + tiles - 1) / tiles;
+  long long maxs = (d.P + 63) / 64;
   if (ns > maxs) ns = maxs;
   if (ns < 1) ns = 1;
   long long pps = (d.P + ns - 1) / ns;
@@ -263,7 +331,10 @@ size_t wg_plan(WgDesc& d) {
   d.nsplit = (int)((d.P + pps - 1) / pps);
   if (d.nsplit < 1) d.nsplit = 1;
   const int Tp = d.generic ? 1 : d.T;
-  return (size_t)d.nsplit * Tp * (size_t)d.Cg * d.ncols * sizeof(float);
+  const size_t slab = (size_t)d.nsplit * Tp * (size_t)d.Cg * d.ncols * sizeof(float);
+  const int G = (d.nsplit + WG_SPG - 1) / WG_SPG;
+  const size_t lvl2 = G > 1 ? (size_t)G * d.Cg * d.Cx * d.T * sizeof(float) : 0;
+  return ic_align(slab, 256) + lvl2;
 }
 
 int wg_run(WgDesc& d, hipStream_t s) {
@@ -277,15 +348,25 @@ int wg_run(WgDesc& d, hipStream_t s) {
 
 int wg_reduce(const WgDesc& d, float* out, const int* kk_of_t, int kk, hipStream_t s) {
   WgRed r;
-  r.partial = d.partial; r.out = out; r.nsplit = d.nsplit; r.Tp = d.generic ? 1 : d.T; r.T = d.T;
+  r.partial = d.partial; r.nsplit = d.nsplit; r.Tp = d.generic ? 1 : d.T; r.T = d.T;
   r.Cg = d.Cg; r.Cx = d.Cx; r.ncols = d.ncols; r.kk = kk; r.generic = d.generic;
+  r.spg = WG_SPG;
+  r.G = (d.nsplit + WG_SPG - 1) / WG_SPG;
   for (int t = 0; t < d.T; ++t) r.kk_of_t[t] = kk_of_t[t];
   const long long total = (long long)d.Cg * d.Cx * d.T;
+  const size_t slab = (size_t)d.nsplit * r.Tp * (size_t)d.Cg * d.ncols * sizeof(float);
+  float* p2 = (float*)((char*)d.partial + ic_align(slab, 256));
+  r.out = r.G == 1 ? out : p2;
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) return IC_OK;
-  hipLaunchKernelGGL(wg_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, r);
+  hipLaunchKernelGGL(wg_reduce_kernel, dim3((unsigned)blocks, r.G), dim3(256), 0, s, r);
   IC_CHECK_LAUNCH();
+  if (r.G > 1) {
+    hipLaunchKernelGGL(wg_reduce2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p2, r.G, total, d.Cx, d.T, kk,
+                       r, out);
+    IC_CHECK_LAUNCH();
+  }
   return IC_OK;
 }
 
@@ -299,10 +380,15 @@ int colsum(const float* t, long long s_n, long long s_c, long long s_h, long lon
   const int nb = colsum_blocks(rows);
   const long long rpb = (rows + nb - 1) / nb;
   float* part = (float*)ws;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s, t, s_n, s_c, s_h, s_w, N, C, H,
-                     W, rows, rpb, part);
+  const bool nhwc = s_c == 1 && s_w == C && s_h == (long long)W * C && s_n == (long long)H * W * C;
+  if (nhwc && C % 4 == 0 && C / 4 <= 256 && (C / 4) * (256 / (C / 4)) * 4 <= 8192) {
+    hipLaunchKernelGGL(colsum_rows_kernel, dim3(nb), dim3(256), 0, s, t, rows, C, rpb, part);
+  } else {
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s, t, s_n, s_c, s_h, s_w, N, C, H,
+                       W, rows, rpb, part);
+  }
   IC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nb, C, scale, out);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, nb, C, scale, out);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
