@@ -58,6 +58,13 @@ void gemm1x1(IgDesc& d, const ic_act* x, const ic_act* y) {
 
 int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inverse,
                  const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+  const long long P = (long long)x->n * x->h * x->w;
+  // the workspace query answers for the general path (the fused one needs none)
+  if (!need && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
+      x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
+      ((uintptr_t)gamma & 15) == 0) {
+    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s);
+  }
   IgDesc d = {};
   gemm1x1(d, x, y);
   d.bias = beta;
@@ -85,6 +92,14 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
                  size_t* need) {
   const long long n = act_numel(x);
+  const long long P = (long long)x->n * x->h * x->w;
+  // fused path: x, dx, norm, dy all NHWC-dense with x's strides; its workspace
+  // (per-block dgamma partials) is also reserved by the query below
+  const size_t fused_ws = gdn_bwd_fused_ws(x->c, P);
+  if (!need && gdn_fused_ok(x->data, dx->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
+      ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
+      wsb >= fused_ws)
+    return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s);
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};
@@ -104,7 +119,7 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
   const size_t cs = colsum_ws((long long)x->n * x->h * x->w, x->c);
   const size_t tot = ic_align((size_t)n * 4, 256) + ic_align(wpb, 256) + ic_align(part, 256) +
                      ic_align(wpart, 256) + ic_align(cs, 256);
-  if (need) { *need = tot; return IC_OK; }
+  if (need) { *need = tot > fused_ws ? tot : fused_ws; return IC_OK; }
   if (!dense_like(x)) return IC_ERR_ARG;
   if (x->sn != dx->sn || x->sc != dx->sc || x->sh != dx->sh || x->sw != dx->sw) return IC_ERR_ARG;
   if (wsb < tot) return IC_ERR_WORKSPACE;

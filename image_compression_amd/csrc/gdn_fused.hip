@@ -1,0 +1,453 @@
+// Fused GDN / IGDN forward and backward for NHWC-dense activations with
+// C in {64, 128, 192} (modelling/layers/gdn.py:79-88):
+//
+//   norm[m][n] = beta[n] + sum_k gamma[n][k] * x[m][k]^2
+//   y[m][n]    = x[m][n] * norm^-1/2            (IGDN: x * norm^1/2)
+//
+// backward (q = dL/dnorm):
+//   q[m][n]      = -1/2 dy x norm^-3/2         (IGDN: +1/2 dy x norm^-1/2)
+//   dx[m][k]     = dy norm^-1/2 (IGDN: dy norm^1/2) + 2 x[m][k] sum_n q[m][n] gamma[n][k]
+//   dgamma[n][k] = sum_m q[m][n] x[m][k]^2,  dbeta[n] = sum_m q[m][n]
+//
+// Both are persistent kernels: 4 waves per block, wave w owns a C/4 slice of
+// output channels and keeps its slice of gamma as MFMA B fragments in VGPRs for
+// the whole launch, so gamma is read once per block.  Pixel tiles (BM rows of
+// one contiguous NHWC run) stream in by LDS-DMA (global_load_lds_dwordx4) into
+// two LDS buffers so tile i+1 lands while tile i computes.  Tile images are
+// [row][C] with the 16-B chunks XOR-swizzled by row (chunk ^ (row & 15)) so the
+// 16 rows of an MFMA fragment read distinct banks; the swizzle is applied to
+// the DMA *source* address because the LDS-DMA destination is lane-linear.
+// Results are written back into LDS and leave through one coalesced copy-out
+// pass (whole 16-B chunks), so every HBM byte moves once:
+//   fwd: read x, write y and norm               (3 C 4 B per pixel)
+//   bwd: read x, norm, dy, write dx             (4 C 4 B per pixel)
+// The backward also accumulates dgamma (C x C) in VGPRs across all of the
+// block's tiles and writes one partial per block; a fixed-order reduction
+// kernel sums the partials (deterministic, no atomics).
+//
+// MFMA: v_mfma_f32_16x16x4_f32 (exact f32).  Where an operand comes from a
+// b128 LDS read, step s = 4u+v consumes logical channel 16u + 4*(lane>>4) + v in
+// both operands.
+#include "../../include/imgcomp.h"
+#include "gemm.h"
+
+namespace {
+
+__device__ __attribute__((aligned(16))) float gdn_zero_page[4];
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+}
+
+// element (m, n) of a swizzled [rows][C] tile image
+template <int C>
+__device__ __forceinline__ int swz(int m, int n) {
+  return m * C + ((((n >> 2) ^ (m & 15)) << 2) | (n & 3));
+}
+
+// stage rows [m0, m0+BM) of a dense [P][C] tensor into a swizzled LDS image
+template <int C, int BM, int NT>
+__device__ __forceinline__ void stage_tile(const float* __restrict__ g, uint32_t m0, uint32_t P, float* img, int tid,
+                                           int lane) {
+  constexpr int CH = C / 4;
+  constexpr int QPASS = BM * CH / NT;
+  static_assert(BM * CH % NT == 0, "whole DMA passes");
+#pragma unroll
+  for (int q = 0; q < QPASS; ++q) {
+    const int pos = tid + NT * q;  // lane-linear LDS chunk
+    const int row = pos / CH, pc = pos - (pos / CH) * CH;
+    const int lc = pc ^ (row & 15);  // logical chunk stored at pc
+    const float* src = gdn_zero_page;
+    if (m0 + row < P) src = g + (size_t)(m0 + row) * C + lc * 4;
+    glds16(src, img + (pos - lane) * 4);
+  }
+}
+
+// copy a swizzled LDS image out to rows [m0, m0+BM) of a dense [P][C] tensor
+template <int C, int BM, int NT>
+__device__ __forceinline__ void store_tile(float* __restrict__ g, uint32_t m0, uint32_t P, const float* img, int tid) {
+  constexpr int CH = C / 4;
+  constexpr int QPASS = BM * CH / NT;
+#pragma unroll
+  for (int q = 0; q < QPASS; ++q) {
+    const int pos = tid + NT * q;
+    const int row = pos / CH, lc = pos - (pos / CH) * CH;
+    const floatx4v v = *(const floatx4v*)(img + row * C + ((lc ^ (row & 15)) << 2));
+    if (m0 + row < P) *(floatx4v*)(g + (size_t)(m0 + row) * C + lc * 4) = v;
+  }
+}
+
+// ============================================================== forward
+// 4 waves (one per SIMD, whole register file): wave w computes n-slice w of
+// every row of the tile.
+template <int C, int BM>
+__global__ void __launch_bounds__(256, 1)
+    gdn_fwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                         const float* __restrict__ beta, int inverse, float* __restrict__ y,
+                         float* __restrict__ norm, uint32_t P) {
+  constexpr int NT = 256;
+  constexpr int NTW = C / 64;    // 16-wide n-tiles per wave
+  constexpr int KU = C / 16;     // groups of 4 k-steps
+  constexpr int MT = BM / 16;    // 16-row m-tiles per wave
+  constexpr int TILE = BM * C;
+  constexpr int NSTORE = 2 * (BM * C / 4 / NT);  // vector-memory ops of one copy-out
+  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];  // 2 x-buffers + norm staging
+  float* const nst = lds + 2 * TILE;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int nbase = w * (C / 4);
+  constexpr int mbase = 0;
+  const uint32_t ntiles = (P + BM - 1) / BM;
+
+  // bfr[j][4u+v] = gamma[n = nbase+16j+li][k = 16u+4lq+v]
+  float bfr[NTW][4 * KU];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const floatx4v g4 = *(const floatx4v*)(gamma + (size_t)(nbase + 16 * j + li) * C + 16 * u + 4 * lq);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bfr[j][4 * u + v] = g4[v];
+    }
+  float bet[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) bet[j] = beta[nbase + 16 * j + li];
+
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) stage_tile<C, BM, NT>(x, tile * BM, P, lds, tid, lane);
+  int buf = 0;
+  bool first = true;
+  for (; tile < ntiles; tile += gridDim.x) {
+    // tile `buf` landed: its DMA is older than the previous copy-out's stores
+    if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+    __builtin_amdgcn_s_barrier();
+    first = false;
+    const uint32_t nxt = tile + gridDim.x;
+    if (nxt < ntiles) stage_tile<C, BM, NT>(x, nxt * BM, P, lds + (buf ^ 1) * TILE, tid, lane);
+    float* xs = lds + buf * TILE;
+
+    floatx4v acc[MT][NTW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[mt][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      floatx4v a4[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        a4[mt] = *(const floatx4v*)(xs + (mbase + 16 * mt + li) * C + (((4 * u + lq) ^ li) << 2));
+        a4[mt] = a4[mt] * a4[mt];
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[mt][v], bfr[j][4 * u + v], acc[mt][j], 0, 0, 0);
+    }
+    // every wave's x^2 reads are done before y overwrites x in place
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // epilogue into LDS (C/D map: col n = li, row m = 4*lq + r); y in place of x
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = nbase + 16 * j + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int off = swz<C>(mbase + 16 * mt + 4 * lq + r, n);
+          const float nv = acc[mt][j][r] + bet[j];
+          const float xv = xs[off];
+          xs[off] = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
+          nst[off] = nv;
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    store_tile<C, BM, NT>(y, tile * BM, P, xs, tid);
+    store_tile<C, BM, NT>(norm, tile * BM, P, nst, tid);
+    buf ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ============================================================== backward
+// phase A of one tile (elementwise, identical swizzled offsets in every image):
+// q = dL/dnorm, and the direct term dy*norm^-1/2 (IGDN: dy*norm^1/2) over dy
+template <int C, int BM>
+__device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
+                                                uint32_t P, int inverse, int tid) {
+  constexpr int NCH = BM * C / 4;
+  for (int pos = tid; pos < NCH; pos += 512) {
+    const int off = pos * 4;
+    const bool valid = m0 + (uint32_t)(pos / (C / 4)) < P;  // rows past P are zero-filled
+    const floatx4v xv = *(const floatx4v*)(xs + off);
+    const floatx4v nv = *(const floatx4v*)(ns + off);
+    const floatx4v gv = *(const floatx4v*)(gs + off);
+    floatx4v qv, dv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rs = __builtin_amdgcn_rsqf(nv[e]);
+      if (inverse) {
+        qv[e] = 0.5f * gv[e] * xv[e] * rs;
+        dv[e] = gv[e] * (nv[e] * rs);
+      } else {
+        qv[e] = -0.5f * gv[e] * xv[e] * (rs * rs * rs);
+        dv[e] = gv[e] * rs;
+      }
+    }
+    if (!valid) {  // keep 0 * inf out of dgamma
+      qv = floatx4v{0.f, 0.f, 0.f, 0.f};
+      dv = qv;
+    }
+    *(floatx4v*)(qs + off) = qv;
+    *(floatx4v*)(gs + off) = dv;
+  }
+}
+
+__device__ __forceinline__ void bar_wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// 8 waves, specialised (two per SIMD): waves 0-3 (group A) stage the tiles,
+// form dx by a GEMM with gamma held in VGPRs and copy it out; waves 4-7
+// (group B) accumulate dgamma (C x C, in VGPRs) and dbeta.  The groups run
+// separate loops with the same barrier sequence per tile (B1 top, B2 after
+// phase A, B3 before the copy-out), so each keeps only its own registers.
+template <int C>
+__global__ void __launch_bounds__(512, 2)
+    gdn_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
+                         const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
+                         float* __restrict__ slab, uint32_t P) {
+  constexpr int BM = 16;
+  constexpr int NTA = 256;       // threads of group A (staging / copy-out)
+  constexpr int W4 = C / 4;      // channels per wave slice
+  constexpr int NTW = C / 64;    // 16-wide tiles per wave slice
+  constexpr int KT = C / 16;     // 16-wide tiles over all channels
+  constexpr int KU = C / 16;
+  constexpr int TILE = BM * C;
+  constexpr int NSTORE = BM * C / 4 / NTA;
+  // per buffer: x, norm, dy images; plus the q image
+  __shared__ __attribute__((aligned(16))) float lds[7 * TILE];
+  float* const qs = lds + 6 * TILE;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int wbase = (w & 3) * W4;
+  const uint32_t ntiles = (P + BM - 1) / BM;
+
+  if (w < 4) {
+    // ---------------- group A: dxg[m][k] = sum_n q[m][n] gamma[n][k], k = wbase + 16j + li
+    // step s = 4u+v: n = 16u + 4lq + v  ->  bfr[j][4u+v] = gamma[n][k]
+    float bfr[NTW][4 * KU];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          bfr[j][4 * u + v] = gamma[(size_t)(16 * u + 4 * lq + v) * C + wbase + 16 * j + li];
+    auto stage = [&](uint32_t t, int b) {
+      float* base = lds + b * 3 * TILE;
+      stage_tile<C, BM, NTA>(x, t * BM, P, base, tid, lane);
+      stage_tile<C, BM, NTA>(norm, t * BM, P, base + TILE, tid, lane);
+      stage_tile<C, BM, NTA>(dy, t * BM, P, base + 2 * TILE, tid, lane);
+    };
+    uint32_t tile = blockIdx.x;
+    if (tile < ntiles) stage(tile, 0);
+    int buf = 0;
+    bool first = true;
+    for (; tile < ntiles; tile += gridDim.x) {
+      if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      __builtin_amdgcn_s_barrier();  // B1
+      first = false;
+      const uint32_t nxt = tile + gridDim.x;
+      if (nxt < ntiles) stage(nxt, buf ^ 1);
+      float* xs = lds + buf * 3 * TILE;
+      float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
+      gdn_bwd_phase_a<C, BM>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid);
+      bar_wait_lgkm();  // B2
+      floatx4v acc[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const floatx4v a4 = *(const floatx4v*)(qs + li * C + (((4 * u + lq) ^ li) << 2));
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[v], bfr[j][4 * u + v], acc[j], 0, 0, 0);
+      }
+      // dx = direct + 2 x dxg over the direct term (each element owned by one lane); m = 4lq + r
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int k = wbase + 16 * j + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int off = swz<C>(4 * lq + r, k);
+          gs[off] = gs[off] + 2.f * xs[off] * acc[j][r];
+        }
+      }
+      bar_wait_lgkm();  // B3
+      store_tile<C, BM, NTA>(dx, tile * BM, P, gs, tid);
+      buf ^= 1;
+    }
+  } else {
+    // ---------------- group B: dgamma[n][k] += sum_m q[m][n] x[m][k]^2, rows n = wbase + 16i + li
+    floatx4v dg[NTW][KT];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) dg[i][kt] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    float db = 0.f;  // dbeta[t] partial, t = tid - 256 < C
+    const int t = tid - 256;
+    int buf = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // B1
+      const float* xs = lds + buf * 3 * TILE;
+      const uint32_t m0 = tile * BM;
+      gdn_bwd_phase_a<C, BM>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid);
+      bar_wait_lgkm();  // B2
+      if (t < C) {
+        const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
+        for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < BM / 4; ++s2) {
+        const int m = 4 * s2 + lq;  // k-step s2 of the pixel reduction
+        float a[NTW];
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) a[i] = qs[swz<C>(m, wbase + 16 * i + li)];
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          float b = xs[swz<C>(m, 16 * kt + li)];
+          b = b * b;
+#pragma unroll
+          for (int i = 0; i < NTW; ++i)
+            dg[i][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b, dg[i][kt], 0, 0, 0);
+        }
+      }
+      bar_wait_lgkm();  // B3
+      buf ^= 1;
+    }
+    // partials: slab[block][n][k] (C*C) then dbeta [C]
+    float* out = slab + (size_t)blockIdx.x * (C * C + C);
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // C/D map: row (A index n) = 4lq + r, col (B index k) = li
+          const int n = wbase + 16 * i + 4 * lq + r;
+          const int k = 16 * kt + li;
+          out[(size_t)n * C + k] = dg[i][kt][r];
+        }
+    if (t < C) out[C * C + t] = db;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// fixed-order sum of the per-block partials
+__global__ void gdn_slab_reduce_kernel(const float* __restrict__ slab, int nb, int C, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta) {
+  const int stride = C * C + C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += gridDim.x * blockDim.x) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = 0;
+    for (; b + 3 < nb; b += 4) {
+      a0 += slab[(size_t)b * stride + i];
+      a1 += slab[(size_t)(b + 1) * stride + i];
+      a2 += slab[(size_t)(b + 2) * stride + i];
+      a3 += slab[(size_t)(b + 3) * stride + i];
+    }
+    for (; b < nb; ++b) a0 += slab[(size_t)b * stride + i];
+    const float v = (a0 + a1) + (a2 + a3);
+    if (i < C * C) {
+      if (dgamma) dgamma[i] = v;
+    } else if (dbeta) {
+      dbeta[i - C * C] = v;
+    }
+  }
+}
+
+constexpr int FWD_BM = 64;
+
+template <int C>
+int gdn_fwd_fused_launch(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm,
+                         long long P, hipStream_t s) {
+  const long long ntiles = (P + FWD_BM - 1) / FWD_BM;
+  long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
+  if (grid < 1) return IC_OK;
+  hipLaunchKernelGGL((gdn_fwd_fused_kernel<C, FWD_BM>), dim3((unsigned)grid), dim3(256), 0, s, x, gamma, beta,
+                     inverse, y, norm, (uint32_t)P);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int bwd_grid(long long P) {
+  const long long ntiles = (P + 15) / 16;
+  return (int)(ntiles < 256 ? ntiles : 256);
+}
+
+template <int C>
+int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                         float* dx, float* dgamma, float* dbeta, long long P, float* slab, hipStream_t s) {
+  const int grid = bwd_grid(P);
+  if (grid < 1) return IC_OK;
+  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx, slab,
+                     (uint32_t)P);
+  IC_CHECK_LAUNCH();
+  const int stride = C * C + C;
+  hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 255) / 256), dim3(256), 0, s, slab, grid, C, dgamma,
+                     dbeta);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+}  // namespace
+
+// NHWC-dense (channel stride 1, pixel stride C), 16-B aligned, C in {64,128,192}
+bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long long sc, long long sw, long long sh,
+                  long long sn, int H, int W, long long P) {
+  if (!(C == 64 || C == 128 || C == 192)) return false;
+  if (sc != 1 || sw != C || sh != (long long)W * C || sn != (long long)H * W * C) return false;
+  if (P >= (1LL << 31) || P < 1) return false;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return a16(x) && a16(y) && a16(norm);
+}
+
+int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
+                  long long P, hipStream_t s) {
+  switch (C) {
+    case 64: return gdn_fwd_fused_launch<64>(x, gamma, beta, inverse, y, norm, P, s);
+    case 128: return gdn_fwd_fused_launch<128>(x, gamma, beta, inverse, y, norm, P, s);
+    case 192: return gdn_fwd_fused_launch<192>(x, gamma, beta, inverse, y, norm, P, s);
+    default: return IC_ERR_ARG;
+  }
+}
+
+size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * (C * C + C) * sizeof(float); }
+
+int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s) {
+  float* slab = (float*)ws;
+  switch (C) {
+    case 64: return gdn_bwd_fused_launch<64>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
+    case 128: return gdn_bwd_fused_launch<128>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
+    case 192: return gdn_bwd_fused_launch<192>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
+    default: return IC_ERR_ARG;
+  }
+}

@@ -78,6 +78,7 @@ struct WgDesc {
   int mtiles, ntiles;
   long long P;     // N*Hg*Wg
   int pps, nsplit; // pixels per split, number of splits
+  FastDiv fd_hw, fd_w;  // divide a pixel index by Hg*Wg and by Wg (set by wg_run)
   float* partial;  // [nsplit][Tp][Cg][ncols]
   int dy[IC_MAXT], dx[IC_MAXT];
 };
@@ -107,3 +108,12 @@ int im2col_run(const float* x, long long sn, long long sc, long long sh, long lo
 int col2im_run(const float* ycol, int ncol, int N, int Hi, int Wi, const float* bias, float* y, long long sn,
                long long sc, long long sh, long long sw, int B, int Ho, int Wo, int k, int stride, int pad,
                int act, hipStream_t s);
+
+// fused GDN (gdn_fused.hip): NHWC-dense, C in {64,128,192}
+bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long long sc, long long sw, long long sh,
+                  long long sn, int H, int W, long long P);
+int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
+                  long long P, hipStream_t s);
+size_t gdn_bwd_fused_ws(int C, long long P);
+int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s);

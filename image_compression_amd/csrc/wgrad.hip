@@ -26,36 +26,52 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
   __shared__ __attribute__((aligned(16))) float Gs[BK * BM];
   __shared__ __attribute__((aligned(16))) float Xs[BK * BN];
 
+  // XCD-aware work order: hardware places block b on XCD b % 8; consecutive
+  // work items (the taps / tiles of one pixel split, which share G and X rows)
+  // are given to blocks of the same XCD so those rows are reused in its L2.
+  const int Tp = GEN ? 1 : d.T;
   const int tiles = d.mtiles * d.ntiles;
-  const int bx = blockIdx.x;
+  const int nblk = tiles * Tp * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int per_split = tiles * Tp;
+  const int split = wid / per_split;
+  const int bx = wid - split * per_split;
   const int t = GEN ? 0 : bx / tiles;
   const int rem = bx - t * tiles;
   const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
   const int g0 = mt * BM, c0 = nt * BN;
-  const int split = blockIdx.y;
-  const long long pb = (long long)split * d.pps;
-  long long pe = pb + d.pps;
-  if (pe > d.P) pe = d.P;
-  const long long HW = (long long)d.Hg * d.Wg;
+  const uint32_t pb = (uint32_t)split * (uint32_t)d.pps;
+  uint32_t pe = pb + (uint32_t)d.pps;
+  if (pe > (uint32_t)d.P) pe = (uint32_t)d.P;
   const int tid = threadIdx.x;
   const int dyt = GEN ? 0 : d.dy[t], dxt = GEN ? 0 : d.dx[t];
 
   floatx4v rg[GPASS], rx[XPASS];
 
-  auto gload = [&](long long p0) {
+  // pixel p -> (img, gy, gx) with 32-bit magic division (P < 2^31)
+  auto pix = [&](uint32_t p, uint32_t& img, int& gy, int& gx) {
+    img = fdiv(p, d.fd_hw);
+    const uint32_t rr = p - img * d.fd_hw.d;
+    const uint32_t y = fdiv(rr, d.fd_w);
+    gy = (int)y;
+    gx = (int)(rr - y * d.fd_w.d);
+  };
+
+  auto gload = [&](uint32_t p0) {
 #pragma unroll
     for (int q = 0; q < GPASS; ++q) {
       const int f = tid + 256 * q;
       floatx4v v = {0.f, 0.f, 0.f, 0.f};
       if (f < BK * G4) {
         const int row = f / G4, c4 = f - (f / G4) * G4;
-        const long long p = p0 + row;
+        const uint32_t p = p0 + row;
         const int col = g0 + c4 * 4;
         if (p < pe && col < d.Cg) {
-          const long long img = p / HW;
-          const long long rr = p - img * HW;
-          const int gy = (int)(rr / d.Wg), gx = (int)(rr - (long long)(rr / d.Wg) * d.Wg);
-          const float* gp = d.g + img * d.gs_n + (long long)gy * d.gs_h + (long long)gx * d.gs_w;
+          uint32_t img; int gy, gx;
+          pix(p, img, gy, gx);
+          const float* gp = d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx * d.gs_w;
           if (d.g_vec) {
             v = *(const floatx4v*)(gp + col);
           } else {
@@ -74,16 +90,16 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
       floatx4v v = {0.f, 0.f, 0.f, 0.f};
       if (f < BK * X4) {
         const int row = f / X4, c4 = f - (f / X4) * X4;
-        const long long p = p0 + row;
+        const uint32_t p = p0 + row;
         if (p < pe) {
-          const long long img = p / HW;
-          const long long rr = p - img * HW;
-          const int gy = (int)(rr / d.Wg), gx = (int)(rr - (long long)(rr / d.Wg) * d.Wg);
+          uint32_t img; int gy, gx;
+          pix(p, img, gy, gx);
           if constexpr (!GEN) {
             const int col = c0 + c4 * 4;
             const int iy = gy * d.stride + dyt, ix = gx * d.stride + dxt;
             if (col < d.Cx && (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx) {
-              v = *(const floatx4v*)(d.x + img * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w + col);
+              v = *(const floatx4v*)(d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h +
+                                     (long long)ix * d.xs_w + col);
               if (d.x_op == AOP_SQUARE) v = v * v;
             }
           } else {
@@ -96,7 +112,8 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
               if (tt < d.T) {
                 const int iy = gy * d.stride + d.dy[tt], ix = gx * d.stride + d.dx[tt];
                 if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx) {
-                  val = d.x[img * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w + (long long)cx * d.xs_c];
+                  val = d.x[(long long)img * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w +
+                            (long long)cx * d.xs_c];
                   if (d.x_op == AOP_SQUARE) val *= val;
                 }
               }
@@ -138,29 +155,161 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
     sstore();
   }
   __syncthreads();
-  for (long long p0 = pb; p0 < pe; p0 += BK) {
-    if (p0 + BK < pe) gload(p0 + BK);
+  for (uint32_t p0 = pb; p0 < pe; p0 += BK) {
+    const bool more = p0 + BK < pe;
+    if (more) gload(p0 + BK);
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s) {
       const int k = 2 * s + h;
-      float a[TM], b[TN];
+      float a[TM], bb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) a[i] = Gs[k * BM + wm * WM + i * 32 + r];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Xs[k * BN + wn * WN + j * 32 + r];
+      for (int j = 0; j < TN; ++j) bb[j] = Xs[k * BN + wn * WN + j * 32 + r];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
-    if (p0 + BK < pe) sstore();
+    if (more) sstore();
     __syncthreads();
   }
 
-  const int Tp = GEN ? 1 : d.T;
   float* slab = d.partial + ((long long)split * Tp + t) * (long long)d.Cg * d.ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int gr = g0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (gr >= d.Cg) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = c0 + wn * WN + j * 32 + r;
+        if (col < d.ncols) slab[(long long)gr * d.ncols + col] = acc[i][j][reg];
+      }
+    }
+}
+
+// Fast path (G and X channel-contiguous, 4-channel aligned): both operand
+// tiles are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
+// round trip) into two LDS buffers, so tile i+1 streams in while the MFMAs
+// consume tile i; one barrier per 16-pixel K-step.  The LDS image is exactly
+// lane-linear ([k][m] rows, no padding) as LDS-DMA requires; out-of-range rows
+// (past the split, outside the image = zero padding) read a zero page.
+__device__ __attribute__((aligned(16))) float wg_zero_page[4];
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
+  constexpr int BK = 16;
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int G4 = BM / 4, X4 = BN / 4;
+  constexpr int GPASS = BK * G4 / 256, XPASS = BK * X4 / 256;
+  static_assert(BK * G4 % 256 == 0 && BK * X4 % 256 == 0, "whole LDS-DMA passes");
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  constexpr int STAGE = BK * (BM + BN);
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+  const int tiles = d.mtiles * d.ntiles;
+  const int nblk = tiles * d.T * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int per_split = tiles * d.T;
+  const int split = wid / per_split;
+  const int bx = wid - split * per_split;
+  const int t = bx / tiles;
+  const int rem = bx - t * tiles;
+  const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
+  const int g0 = mt * BM, c0 = nt * BN;
+  const uint32_t pb = (uint32_t)split * (uint32_t)d.pps;
+  uint32_t pe = pb + (uint32_t)d.pps;
+  if (pe > (uint32_t)d.P) pe = (uint32_t)d.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dyt = d.dy[t], dxt = d.dx[t];
+
+  auto stage = [&](uint32_t p0, int buf) {
+    float* Gs = lds + buf * STAGE;
+    float* Xs = Gs + BK * BM;
+#pragma unroll
+    for (int q = 0; q < GPASS; ++q) {
+      const int f = tid + 256 * q;
+      const int row = f / G4, c4 = f - (f / G4) * G4;
+      const uint32_t p = p0 + row;
+      const int col = g0 + c4 * 4;
+      const float* src = wg_zero_page;
+      if (p < pe && col < d.Cg) {
+        const uint32_t img = fdiv(p, d.fd_hw);
+        const uint32_t rr = p - img * d.fd_hw.d;
+        const uint32_t gy = fdiv(rr, d.fd_w);
+        const uint32_t gx = rr - gy * d.fd_w.d;
+        src = d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx * d.gs_w + col;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Gs + (f - lane) * 4), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < XPASS; ++q) {
+      const int f = tid + 256 * q;
+      const int row = f / X4, c4 = f - (f / X4) * X4;
+      const uint32_t p = p0 + row;
+      const int col = c0 + c4 * 4;
+      const float* src = wg_zero_page;
+      if (p < pe && col < d.Cx) {
+        const uint32_t img = fdiv(p, d.fd_hw);
+        const uint32_t rr = p - img * d.fd_hw.d;
+        const uint32_t gy = fdiv(rr, d.fd_w);
+        const uint32_t gx = rr - gy * d.fd_w.d;
+        const int iy = (int)gy * d.stride + dyt, ix = (int)gx * d.stride + dxt;
+        if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)
+          src = d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w + col;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Xs + (f - lane) * 4), 16, 0, 0);
+    }
+  };
+
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 31, h = lane >> 5;
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (pb < pe) stage(pb, 0);
+  int buf = 0;
+  for (uint32_t p0 = pb; p0 < pe; p0 += BK) {
+    __syncthreads();  // tile `buf` landed (vmcnt(0) + barrier); everyone is done with buf^1
+    if (p0 + BK < pe) stage(p0 + BK, buf ^ 1);
+    const float* Gs = lds + buf * STAGE;
+    const float* Xs = Gs + BK * BM;
+    const bool x_sq = d.x_op == AOP_SQUARE;
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int k = 2 * s + h;
+      float a[TM], bb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = Gs[k * BM + wm * WM + i * 32 + r];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float v = Xs[k * BN + wn * WN + j * 32 + r];
+        bb[j] = x_sq ? v * v : v;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bb[j], acc[i][j], 0, 0, 0);
+    }
+    buf ^= 1;
+  }
+
+  float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -233,8 +382,16 @@ __global__ void wg_reduce2_kernel(const float* p2, int G, long long total, int C
 template <int BM, int BN, int WM, int WN, bool GEN>
 int wg_launch_t(const WgDesc& d, hipStream_t s) {
   const int Tp = GEN ? 1 : d.T;
-  dim3 grid(d.mtiles * d.ntiles * Tp, d.nsplit);
+  dim3 grid((d.mtiles * d.ntiles * Tp * d.nsplit + 7) / 8 * 8);
   hipLaunchKernelGGL((wg_kernel<BM, BN, WM, WN, GEN>), grid, dim3(256), 0, s, d);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+template <int BM, int BN, int WM, int WN>
+int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
+  dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
+  hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
@@ -257,6 +414,31 @@ __global__ void colsum_partial_kernel(const float* t, long long s_n, long long s
     }
     part[(long long)blockIdx.x * C + c] = acc;
   }
+}
+
+// Planar form (NCHW with contiguous H*W planes, e.g. the 3-channel image
+// gradient): block (chunk, c, n) sums one contiguous run of a plane with
+// float4 loads and a fixed-order block reduction.
+__global__ void __launch_bounds__(256) colsum_planes_kernel(const float* t, long long s_n, long long s_c, int C,
+                                                            int HW, int chunk, int nchunk, float* part) {
+  __shared__ float lds[16];
+  const int ck = blockIdx.x, c = blockIdx.y, n = blockIdx.z;
+  const float* base = t + (long long)n * s_n + (long long)c * s_c;
+  const int b0 = ck * chunk;
+  const int b1 = min(HW, b0 + chunk);
+  float acc[1] = {0.f};
+  if (((uintptr_t)base & 15) == 0 && (b0 & 3) == 0) {
+    const int n4 = (b1 - b0) >> 2;
+    const floatx4v* p4 = (const floatx4v*)(base + b0);
+    floatx4v a = {0.f, 0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < n4; i += 256) a += p4[i];
+    acc[0] = (a[0] + a[1]) + (a[2] + a[3]);
+    for (int i = b0 + 4 * n4 + threadIdx.x; i < b1; i += 256) acc[0] += base[i];
+  } else {
+    for (int i = b0 + threadIdx.x; i < b1; i += 256) acc[0] += base[i];
+  }
+  block_sum<1>(acc, lds);
+  if (threadIdx.x == 0) part[((long long)n * nchunk + ck) * C + c] = acc[0];
 }
 
 // NHWC-dense form: rows x C, float4 per thread, rows interleaved over the
@@ -320,13 +502,15 @@ size_t wg_plan(WgDesc& d) {
   d.ntiles = ic_cdiv(d.ncols, d.bn);
   d.P = (long long)d.N * d.Hg * d.Wg;
   const long long tiles = (long long)d.mtiles * d.ntiles * (d.generic ? 1 : d.T);
-  // ~2 resident blocks per CU; never fewer than 64 pixels per split
-  long long ns = (512 + tiles - 1) / tiles;
+  // one full wave of blocks: 256 CUs x 2 resident blocks = 512 slots, so a
+  // grid of just over 512 equal blocks would run at half speed; never fewer
+  // than 64 pixels per split
+  long long ns = tiles >= 512 ? 1 : 512 / tiles;
   long long maxs = (d.P + 63) / 64;
   if (ns > maxs) ns = maxs;
   if (ns < 1) ns = 1;
   long long pps = (d.P + ns - 1) / ns;
-  pps = (pps + 15) / 16 * 16;
+  pps = (pps + 31) / 32 * 32;
   d.pps = (int)pps;
   d.nsplit = (int)((d.P + pps - 1) / pps);
   if (d.nsplit < 1) d.nsplit = 1;
@@ -339,9 +523,20 @@ size_t wg_plan(WgDesc& d) {
 
 int wg_run(WgDesc& d, hipStream_t s) {
   if (d.P == 0) return IC_OK;
+  if (d.P >= (1LL << 31)) return IC_ERR_ARG;  // 32-bit pixel indexing
+  d.fd_hw = make_fastdiv((uint32_t)((long long)d.Hg * d.Wg));
+  d.fd_w = make_fastdiv((uint32_t)d.Wg);
   d.g_vec = (d.gs_c == 1 && d.Cg % 4 == 0);
+  // LDS-DMA path: 16-B aligned float4 rows in both operands
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool glds_ok = d.g_vec && !d.generic && a16(d.g) && a16(d.x) && d.gs_w % 4 == 0 && d.gs_h % 4 == 0 &&
+                       d.gs_n % 4 == 0 && d.xs_w % 4 == 0 && d.xs_h % 4 == 0 && d.xs_n % 4 == 0;
   if (!d.generic && (d.xs_c != 1 || d.Cx % 4 != 0)) return IC_ERR_ARG;
   if (d.generic) return wg_launch_t<192, 64, 96, 32, true>(d, s);
+  if (glds_ok) {
+    if (d.bn == 192) return wg_glds_launch_t<192, 192, 96, 96>(d, s);
+    return wg_glds_launch_t<192, 64, 96, 32>(d, s);
+  }
   if (d.bn == 192) return wg_launch_t<192, 192, 96, 96, false>(d, s);
   return wg_launch_t<192, 64, 96, 32, false>(d, s);
 }
@@ -381,8 +576,24 @@ int colsum(const float* t, long long s_n, long long s_c, long long s_h, long lon
   const long long rpb = (rows + nb - 1) / nb;
   float* part = (float*)ws;
   const bool nhwc = s_c == 1 && s_w == C && s_h == (long long)W * C && s_n == (long long)H * W * C;
+  const long long HW = (long long)H * W;
+  const bool planar = s_w == 1 && s_h == W && HW >= 1024 && HW < (1LL << 30) && (long long)N * C <= nb;
   if (nhwc && C % 4 == 0 && C / 4 <= 256 && (C / 4) * (256 / (C / 4)) * 4 <= 8192) {
     hipLaunchKernelGGL(colsum_rows_kernel, dim3(nb), dim3(256), 0, s, t, rows, C, rpb, part);
+  } else if (planar) {
+    // about nb blocks in total: chunks per plane = nb / (N*C), >= 1
+    long long nchunk = nb / ((long long)N * C);
+    if (nchunk < 1) nchunk = 1;
+    long long chunk = (HW + nchunk - 1) / nchunk;
+    chunk = (chunk + 1023) / 1024 * 1024;
+    nchunk = (HW + chunk - 1) / chunk;
+    hipLaunchKernelGGL(colsum_planes_kernel, dim3((unsigned)nchunk, C, N), dim3(256), 0, s, t, s_n, s_c, C, (int)HW,
+                       (int)chunk, (int)nchunk, part);
+    IC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, (int)(N * nchunk), C, scale,
+                       out);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
   } else {
     hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s, t, s_n, s_c, s_h, s_w, N, C, H,
                        W, rows, rpb, part);
