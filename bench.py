@@ -111,25 +111,13 @@ def main():
                     help="only warmup+timed steps (for rocprofv3 runs)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
+    from image_compression_amd import distributed as D
     from image_compression_amd import modelling
+    rank, world, dev = D.setup()
+    dist = world > 1
     torch.manual_seed(0)
-    model = modelling.build_model(_cfg()).to(dev).train()
-    if dist:
-        from torch.nn.parallel import DistributedDataParallel as DDP
-        model = DDP(model, device_ids=[local], bucket_cap_mb=12, gradient_as_bucket_view=True,
-                    broadcast_buffers=False)
+    model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev)
+    # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
 
@@ -142,27 +130,20 @@ def main():
     for _ in range(args.warmup):
         losses = step()
     torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
+    D.barrier(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = step()
     torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    bpp = float(losses["bpp"])
-    mse = float(losses["MSE"])
+    D.barrier(dev)
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    avg = D.mean_over_ranks({"bpp": losses["bpp"], "MSE": losses["MSE"]}, dev)
+    bpp, mse = avg["bpp"], avg["MSE"]
     if args.profile_step_only:
         if rank == 0:
             print(json.dumps({"ms_per_step": 1e3 * elapsed / args.steps}))
-        if dist:
-            tdist.destroy_process_group()
+        D.teardown()
         return
 
     images = args.batch * world * args.steps
@@ -191,8 +172,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(rec))
-    if dist:
-        tdist.destroy_process_group()
+    D.teardown()
 
 
 if __name__ == "__main__":
