@@ -66,9 +66,22 @@ def dominant_kernel_roofline(dev, reps=20):
     ms = e0.elapsed_time(e1) / reps
     achieved = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": _pmc_traffic(),
             "kernel": "ig_kernel<128,192,64,96> + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4)}
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC passes (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/*_pmc_dominant.json):
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE.  The algorithmic bytes of
+    the launch are 0.51 GB (input 403 MB, weights 3.7 MB, output 101 MB)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_dominant.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        return round(json.load(fh)["traffic_bytes_per_launch"])
 
 
 def cpu_baseline(seconds_target=12.0):

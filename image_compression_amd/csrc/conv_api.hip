@@ -38,6 +38,20 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
                   const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
   const int T = k * k;
   const int Kp = (int)ic_align((size_t)T * x->c, 32);
+  if ((epi == EPI_NONE || epi == EPI_RELU) && edge_conv_ok(x->c, k, stride, x->sw, y->sc, y->c)) {
+    // patch-gather kernel (edge.hip): no im2col columns in HBM
+    const int Npad = ig_npad(y->c);
+    const size_t wpb = (size_t)Npad * Kp * 4;
+    if (need) { *need = ic_align(wpb, 256); return IC_OK; }
+    if (wsb < wpb) return IC_ERR_WORKSPACE;
+    float* wp = (float*)ws;
+    int ky[IC_MAXT], kx[IC_MAXT];
+    for (int t = 0; t < T; ++t) { ky[t] = t / k; kx[t] = t % k; }
+    int rc = pack_weights(W, y->c, x->c, k, 0, 1, T, ky, kx, Npad, Kp, wp, s);
+    if (rc) return rc;
+    return edge_conv_run(x->data, x->sn, x->sc, x->sh, x->sw, x->n, x->c, x->h, x->w, wp, Kp, bias, k, stride, pad,
+                         y->data, y->sn, y->sc, y->sh, y->sw, y->c, y->h, y->w, epi == EPI_RELU, s);
+  }
   const long long rows = (long long)x->n * y->h * y->w;
   ic_act xc;
   xc.data = nullptr; xc.n = x->n; xc.c = Kp; xc.h = y->h; xc.w = y->w;
@@ -239,6 +253,23 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   int kk_of_t[IC_MAXT];
   for (int t = 0; t < d.T; ++t) {
     d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
+  }
+  // few X channels, wide NHWC G: patch-gather wgrad (edge.hip); the bias
+  // gradient comes from its all-ones column when the bias belongs to G
+  if (X->c <= FEW_CH && edge_wgrad_ok(X->c, k, stride, X->sw, G->data, G->c, G->sc, G->sw, G->sh, G->sn, G->h, G->w)) {
+    const bool db_from_g = db && bias_src->data == G->data;
+    const int Kc = k * k * X->c + (db_from_g ? 1 : 0);
+    const size_t slab = edge_wgrad_ws(G->c, Kc, edge_units(G->n, G->h, G->w));
+    const size_t cs = (db && !db_from_g) ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
+    if (need) { *need = ic_align(slab, 256) + ic_align(cs, 256); return IC_OK; }
+    if (wsb < ic_align(slab, 256) + ic_align(cs, 256)) return IC_ERR_WORKSPACE;
+    int rc = edge_wgrad_run(G->data, G->c, X->data, X->sn, X->sc, X->sh, X->sw, X->n, X->c, X->h, X->w, G->h, G->w,
+                            k, stride, pad, dw, db_from_g ? db : nullptr, ws, s);
+    if (rc) return rc;
+    if (db && !db_from_g)
+      rc = colsum(bias_src->data, bias_src->sn, bias_src->sc, bias_src->sh, bias_src->sw, bias_src->n, bias_src->c,
+                  bias_src->h, bias_src->w, db, 1.f, (char*)ws + ic_align(slab, 256), s);
+    return rc;
   }
   // few X channels: wgrad against xcol = im2col(X) on G's grid (1 tap, K = Kp)
   const bool few = X->c <= FEW_CH;

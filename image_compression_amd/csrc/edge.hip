@@ -1,0 +1,421 @@
+// The two image-edge convolutions (3-channel image <-> 192-channel maps),
+// which dominate no FLOP count but move the largest tensors of the step:
+//
+//   edge_conv  : y[p][n] = bias[n] + sum_k xcol[p][k] * wp[n][k]
+//                conv 3->192 5x5 s2 (g_a.0 forward; also the g_s.6 transposed
+//                conv's dgrad, which is the same direct gather)
+//   edge_wgrad : dW[g][k] = sum_p G[p][g] * xcol[p][k]   (+ bias column)
+//                g_a.0 wgrad (G = dy, X = x) and g_s.6 wgrad (G = x, X = dy)
+//
+// with xcol[p][k], k = t*C + c, the (tap, channel) patch of the few-channel
+// image X (NCHW, rows contiguous) at output pixel p.  Instead of materialising
+// xcol in HBM (im2col: 100 B per pixel written and read back), each work unit
+// = one 64-pixel segment of an output row stages the C x k x (63*s+k) input
+// patch it needs in LDS (zero outside the image) and the MFMA operand for
+// (pixel m, column k) is patch[off_k + s*m] — a table of per-lane offsets.
+//
+// Both kernels are persistent (a few blocks per CU loop over the units) and
+// use v_mfma_f32_16x16x4_f32; wave w owns a C_out/4 channel slice.
+//   edge_conv : weights live in VGPRs as B fragments for the whole launch;
+//               output rows are written NHWC straight from the accumulators.
+//   edge_wgrad: the G tile of the unit (64 pixels x 192 channels, one
+//               contiguous NHWC run) arrives by LDS-DMA (row-swizzled, as in
+//               gdn_fused.hip); dW accumulates in VGPRs across units and each
+//               block writes one partial that a fixed-order kernel reduces.
+//               An extra all-ones column k = T*C turns the same MFMAs into
+//               the bias gradient sum_p G[p][g] when G is dy (conv wgrad).
+#include "../../include/imgcomp.h"
+#include "gemm.h"
+
+namespace {
+
+constexpr int SEG = 64;        // output pixels per work unit (one row segment)
+constexpr int KMAX = 100;      // T*C <= 25 taps x 4 channels
+constexpr int PMAX = 4 * 5 * (63 * 2 + 5);  // patch floats: C x k x (63 s + k)
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __attribute__((aligned(16))) float edge_zero_page[4];
+
+struct EdgeGeom {
+  const float* x;            // few-channel image, NCHW strides (sw == 1)
+  long long sn, sc, sh;
+  int N, C, H, W;            // input image
+  int Ho, Wo;                // output grid
+  int k, stride, pad;
+  int PW;                    // patch row length = (SEG-1)*stride + k
+  int TC;                    // T*C real columns
+  int units_per_row;         // ceil(Wo / SEG)
+  long long units;
+};
+
+// the patch of unit u: patch[(c*k + ky)*PW + j] = x[n][c][iy0+ky][ix0+j] (0 outside
+// the image).  Loaded into registers first (pr) and written to LDS later, so
+// the global-load latency hides behind the current unit's MFMAs.
+constexpr int PREG = (PMAX + 255) / 256;
+
+__device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, long long u, float (&pr)[PREG], int tid) {
+  const int seg = (int)(u % g.units_per_row);
+  const long long r = u / g.units_per_row;
+  const int oy = (int)(r % g.Ho);
+  const int n = (int)(r / g.Ho);
+  const int iy0 = oy * g.stride - g.pad, ix0 = seg * SEG * g.stride - g.pad;
+  const int tot = g.C * g.k * g.PW;
+#pragma unroll
+  for (int q = 0; q < PREG; ++q) {
+    const int i = tid + 256 * q;
+    float v = 0.f;
+    if (i < tot) {
+      const int row = i / g.PW, j = i - (i / g.PW) * g.PW;
+      const int c = row / g.k, ky = row - (row / g.k) * g.k;
+      const int iy = iy0 + ky, ix = ix0 + j;
+      if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+        v = g.x[n * g.sn + c * g.sc + (long long)iy * g.sh + ix];
+    }
+    pr[q] = v;
+  }
+}
+
+__device__ __forceinline__ void edge_patch_store(const EdgeGeom& g, const float (&pr)[PREG], float* patch, int tid) {
+  const int tot = g.C * g.k * g.PW;
+#pragma unroll
+  for (int q = 0; q < PREG; ++q) {
+    const int i = tid + 256 * q;
+    if (i < tot) patch[i] = pr[q];
+  }
+}
+
+// LDS offset of column k inside the patch (pixel 0); columns >= TC read the
+// zero run after the patch; column TC reads the ones run when `ones`
+__device__ __forceinline__ int edge_koff(const EdgeGeom& g, int k, int zero_off, int ones_off, bool ones) {
+  if (k < g.TC) {
+    const int t = k / g.C, c = k - (k / g.C) * g.C;
+    const int ky = t / g.k, kx = t - (t / g.k) * g.k;
+    return (c * g.k + ky) * g.PW + kx;
+  }
+  return (ones && k == g.TC) ? ones_off : zero_off;
+}
+
+// ------------------------------------------------------------------ conv
+// y NHWC (channel stride 1, pixel stride ys_w), Cout = 64*NTW*... : wave slice = Cout/4
+template <int COUT>
+__global__ void __launch_bounds__(256, 2)
+    edge_conv_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
+                     int relu, float* __restrict__ y, long long ys_n, long long ys_h, long long ys_w) {
+  constexpr int NTW = COUT / 64;
+  constexpr int KSMAX = (KMAX + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float lds[2 * (PMAX + 2 * SEG * 2)];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int nbase = w * (COUT / 4);
+  const int KS = (g.TC + 3) / 4;
+  const int PSZ = g.C * g.k * g.PW;
+  const int zero_off = PSZ;  // 2*SEG*stride zeros follow the patch
+  const int bufsz = PMAX + 2 * SEG * 2;
+
+  // weights as B fragments: bfr[j][s] = wp[n = nbase+16j+li][k = 4s+lq]
+  float bfr[NTW][KSMAX];
+  int koff[KSMAX];
+#pragma unroll
+  for (int s = 0; s < KSMAX; ++s) {
+    const int kk = 4 * s + lq;
+    koff[s] = edge_koff(g, kk, zero_off, zero_off, false);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) bfr[j][s] = (s < KS && kk < Kp) ? wp[(size_t)(nbase + 16 * j + li) * Kp + kk] : 0.f;
+  }
+  float bv[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) bv[j] = bias ? bias[nbase + 16 * j + li] : 0.f;
+  // zero runs after both patch buffers
+  for (int i = tid; i < 2 * SEG * 2; i += 256) {
+    lds[PSZ + i] = 0.f;
+    lds[bufsz + PSZ + i] = 0.f;
+  }
+
+  long long u = blockIdx.x;
+  int buf = 0;
+  float pr[PREG];
+  if (u < g.units) {
+    edge_patch_load(g, u, pr, tid);
+    edge_patch_store(g, pr, lds, tid);
+  }
+  for (; u < g.units; u += gridDim.x) {
+    __syncthreads();  // patch `buf` complete; everyone is done with buf^1
+    const long long un = u + gridDim.x;
+    if (un < g.units) edge_patch_load(g, un, pr, tid);
+    const float* patch = lds + buf * bufsz;
+    floatx4v acc[SEG / 16][NTW];
+#pragma unroll
+    for (int mt = 0; mt < SEG / 16; ++mt)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[mt][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KSMAX; ++s) {
+      if (s < KS) {
+#pragma unroll
+        for (int mt = 0; mt < SEG / 16; ++mt) {
+          const float a = patch[koff[s] + g.stride * (16 * mt + li)];
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bfr[j][s], acc[mt][j], 0, 0, 0);
+        }
+      }
+    }
+    // epilogue: C/D map col n = li, row m = 4lq + r
+    const int seg = (int)(u % g.units_per_row);
+    const long long rr = u / g.units_per_row;
+    const int oy = (int)(rr % g.Ho);
+    const int n = (int)(rr / g.Ho);
+    const int ox0 = seg * SEG;
+    float* yb = y + n * ys_n + (long long)oy * ys_h;
+#pragma unroll
+    for (int mt = 0; mt < SEG / 16; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ox = ox0 + 16 * mt + 4 * lq + r;
+        if (ox < g.Wo) {
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) {
+            float v = acc[mt][j][r] + bv[j];
+            if (relu) v = v > 0.f ? v : 0.f;
+            yb[(long long)ox * ys_w + nbase + 16 * j + li] = v;
+          }
+        }
+      }
+    if (un < g.units) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
+    buf ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------ wgrad
+// G NHWC-dense [N][Ho][Wo][CG] (pixel stride CG), 16-B aligned; CG in {64,128,192}
+template <int CG>
+__global__ void __launch_bounds__(256, 1)
+    edge_wgrad_kernel(const EdgeGeom g, const float* __restrict__ G, int Kc, int ones, float* __restrict__ slab) {
+  constexpr int NTW = CG / 64;            // 16-wide g-tiles per wave
+  constexpr int KTMAX = (KMAX + 1 + 15) / 16;
+  constexpr int CH = CG / 4;              // 16-B chunks per G row
+  constexpr int GT = SEG * CG;            // G tile floats
+  constexpr int QP = SEG * CH / 256;      // LDS-DMA pieces per thread
+  constexpr int PB = PMAX + 2 * SEG * 2 + 2 * SEG * 2;  // patch + zero run + ones run
+  __shared__ __attribute__((aligned(16))) float lds[2 * GT + 2 * PB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int gbase = w * (CG / 4);
+  const int KT = (Kc + 15) / 16;
+  const int PSZ = g.C * g.k * g.PW;
+  const int zero_off = PSZ, ones_off = PSZ + 2 * SEG * 2;
+  float* const pbase = lds + 2 * GT;
+
+  int koff[KTMAX];
+#pragma unroll
+  for (int kt = 0; kt < KTMAX; ++kt) koff[kt] = edge_koff(g, 16 * kt + li, zero_off, ones_off, ones != 0);
+  for (int i = tid; i < 2 * SEG * 2; i += 256) {
+    pbase[PSZ + i] = 0.f;
+    pbase[PB + PSZ + i] = 0.f;
+    pbase[ones_off + i] = 1.f;
+    pbase[PB + ones_off + i] = 1.f;
+  }
+  floatx4v acc[NTW][KTMAX];
+#pragma unroll
+  for (int i = 0; i < NTW; ++i)
+#pragma unroll
+    for (int kt = 0; kt < KTMAX; ++kt) acc[i][kt] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  // G rows of unit u: pixels (n, oy, ox0 .. ox0+63) are one contiguous NHWC run
+  auto stage_g = [&](long long u, float* img) {
+    const int seg = (int)(u % g.units_per_row);
+    const long long rr = u / g.units_per_row;
+    const long long p0 = rr * g.Wo + (long long)seg * SEG;     // first pixel (n*Ho + oy)*Wo + ox0
+    const int valid = min(SEG, g.Wo - seg * SEG);
+#pragma unroll
+    for (int q = 0; q < QP; ++q) {
+      const int pos = tid + 256 * q;
+      const int row = pos / CH, pc = pos - (pos / CH) * CH;
+      const int lc = pc ^ (row & 15);
+      const float* src = edge_zero_page;
+      if (row < valid) src = G + (size_t)(p0 + row) * CG + lc * 4;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(img + (pos - lane) * 4), 16, 0, 0);
+    }
+  };
+
+  long long u = blockIdx.x;
+  int buf = 0;
+  float pr[PREG];
+  if (u < g.units) {
+    stage_g(u, lds);
+    edge_patch_load(g, u, pr, tid);
+    edge_patch_store(g, pr, pbase, tid);
+  }
+  for (; u < g.units; u += gridDim.x) {
+    __syncthreads();  // vmcnt(0) + barrier: tile `buf` and its patch are in LDS
+    const long long un = u + gridDim.x;
+    if (un < g.units) {
+      stage_g(un, lds + (buf ^ 1) * GT);
+      edge_patch_load(g, un, pr, tid);
+    }
+    const float* gs = lds + buf * GT;
+    const float* patch = pbase + buf * PB;
+    // k-step s2 of the pixel reduction: pixel m = 4 s2 + lq
+#pragma unroll 4
+    for (int s2 = 0; s2 < SEG / 4; ++s2) {
+      const int m = 4 * s2 + lq;
+      float a[NTW];
+#pragma unroll
+      for (int i = 0; i < NTW; ++i) {
+        const int gc = gbase + 16 * i + li;
+        a[i] = gs[m * CG + ((((gc >> 2) ^ (m & 15)) << 2) | (gc & 3))];
+      }
+#pragma unroll
+      for (int kt = 0; kt < KTMAX; ++kt) {
+        if (kt < KT) {
+          const float b = patch[koff[kt] + g.stride * m];
+#pragma unroll
+          for (int i = 0; i < NTW; ++i) acc[i][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b, acc[i][kt], 0, 0, 0);
+        }
+      }
+    }
+    if (un < g.units) edge_patch_store(g, pr, pbase + (buf ^ 1) * PB, tid);
+    buf ^= 1;
+  }
+  // partial [CG][Kc] of this block (C/D map: row = g index 4lq + r, col = k index li)
+  float* out = slab + (size_t)blockIdx.x * CG * Kc;
+#pragma unroll
+  for (int i = 0; i < NTW; ++i)
+#pragma unroll
+    for (int kt = 0; kt < KTMAX; ++kt)
+      if (kt < KT) {
+        const int kk = 16 * kt + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kk < Kc) out[(size_t)(gbase + 16 * i + 4 * lq + r) * Kc + kk] = acc[i][kt][r];
+      }
+}
+
+// fixed-order sum of the partials, scattered to dW[g][c][ky][kx] (+ db[g] from the ones column)
+__global__ void edge_wgrad_reduce_kernel(const float* __restrict__ slab, int nb, int CG, int Kc, int C, int T,
+                                         float* __restrict__ dw, float* __restrict__ db) {
+  const int total = CG * Kc;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int gg = i / Kc, kk = i - (i / Kc) * Kc;
+    if (kk > T * C || (kk == T * C && !db)) continue;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = 0;
+    for (; b + 3 < nb; b += 4) {
+      a0 += slab[(size_t)b * total + i];
+      a1 += slab[(size_t)(b + 1) * total + i];
+      a2 += slab[(size_t)(b + 2) * total + i];
+      a3 += slab[(size_t)(b + 3) * total + i];
+    }
+    for (; b < nb; ++b) a0 += slab[(size_t)b * total + i];
+    const float v = (a0 + a1) + (a2 + a3);
+    if (kk == T * C) {
+      db[gg] = v;
+    } else {
+      const int t = kk / C, c = kk - (kk / C) * C;
+      dw[((size_t)gg * C + c) * T + t] = v;
+    }
+  }
+}
+
+bool edge_geom(EdgeGeom& g, const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C,
+               int H, int W, int Ho, int Wo, int k, int stride, int pad) {
+  if (sw != 1 || C < 1 || C > 4 || k < 1 || k > 5 || stride < 1 || stride > 2) return false;
+  if (k * k * C > KMAX) return false;
+  g.x = x; g.sn = sn; g.sc = sc; g.sh = sh;
+  g.N = N; g.C = C; g.H = H; g.W = W; g.Ho = Ho; g.Wo = Wo;
+  g.k = k; g.stride = stride; g.pad = pad;
+  g.PW = (SEG - 1) * stride + k;
+  g.TC = k * k * C;
+  g.units_per_row = (Wo + SEG - 1) / SEG;
+  g.units = (long long)N * Ho * g.units_per_row;
+  return g.C * g.k * g.PW <= PMAX;
+}
+
+int edge_grid(long long units, int per_cu) {
+  const long long cap = 256LL * per_cu;
+  return (int)(units < cap ? units : cap);
+}
+
+}  // namespace
+
+// y (NHWC, channel stride 1) = conv(x few-channel, wp [Cout][Kp] with k = t*C + c)
+int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H, int W,
+                  const float* wp, int Kp, const float* bias, int k, int stride, int pad, float* y, long long ys_n,
+                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s) {
+  EdgeGeom g;
+  if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
+  if (ys_c != 1 || Kp < g.TC) return IC_ERR_ARG;
+  const int grid = edge_grid(g.units, 2);
+  if (grid < 1) return IC_OK;
+  switch (Cout) {
+    case 192:
+      hipLaunchKernelGGL(edge_conv_kernel<192>, dim3(grid), dim3(256), 0, s, g, wp, Kp, bias, relu, y, ys_n, ys_h,
+                         ys_w);
+      break;
+    case 128:
+      hipLaunchKernelGGL(edge_conv_kernel<128>, dim3(grid), dim3(256), 0, s, g, wp, Kp, bias, relu, y, ys_n, ys_h,
+                         ys_w);
+      break;
+    case 64:
+      hipLaunchKernelGGL(edge_conv_kernel<64>, dim3(grid), dim3(256), 0, s, g, wp, Kp, bias, relu, y, ys_n, ys_h,
+                         ys_w);
+      break;
+    default:
+      return IC_ERR_ARG;
+  }
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout) {
+  return C >= 1 && C <= 4 && k <= 5 && k * k * C <= KMAX && stride >= 1 && stride <= 2 && sw == 1 && ys_c == 1 &&
+         (Cout == 64 || Cout == 128 || Cout == 192);
+}
+
+// workspace of edge_wgrad_run
+size_t edge_wgrad_ws(int CG, int Kc, long long units) {
+  return (size_t)edge_grid(units, 1) * CG * Kc * sizeof(float);
+}
+
+bool edge_wgrad_ok(int C, int k, int stride, long long sw, const float* G, int CG, long long gs_c, long long gs_w,
+                   long long gs_h, long long gs_n, int Ho, int Wo) {
+  if (!(C >= 1 && C <= 4 && k <= 5 && k * k * C + 1 <= KMAX + 1 && stride >= 1 && stride <= 2 && sw == 1)) return false;
+  if (!(CG == 64 || CG == 128 || CG == 192)) return false;
+  if (gs_c != 1 || gs_w != CG || gs_h != (long long)Wo * CG || gs_n != (long long)Ho * Wo * CG) return false;
+  return ((uintptr_t)G & 15) == 0;
+}
+
+long long edge_units(int N, int Ho, int Wo) { return (long long)N * Ho * ((Wo + SEG - 1) / SEG); }
+
+// dW[g][c][ky][kx] = sum_p G[p][g] X[p*s + tap][c];  db[g] = sum_p G[p][g] when db != NULL
+int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
+                   int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,
+                   void* ws, hipStream_t s) {
+  EdgeGeom g;
+  if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
+  const int Kc = g.TC + (db ? 1 : 0);
+  const int grid = edge_grid(g.units, 1);
+  if (grid < 1) return IC_OK;
+  float* slab = (float*)ws;
+  switch (CG) {
+    case 192:
+      hipLaunchKernelGGL(edge_wgrad_kernel<192>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      break;
+    case 128:
+      hipLaunchKernelGGL(edge_wgrad_kernel<128>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      break;
+    case 64:
+      hipLaunchKernelGGL(edge_wgrad_kernel<64>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      break;
+    default:
+      return IC_ERR_ARG;
+  }
+  IC_CHECK_LAUNCH();
+  const int total = CG * Kc;
+  hipLaunchKernelGGL(edge_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, grid, CG, Kc, C,
+                     k * k, dw, db);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}

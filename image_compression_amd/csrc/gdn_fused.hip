@@ -81,17 +81,23 @@ __device__ __forceinline__ void store_tile(float* __restrict__ g, uint32_t m0, u
 }
 
 // ============================================================== forward
-// 4 waves (one per SIMD, whole register file): wave w computes n-slice w of
-// every row of the tile.
+// NW = C/32 waves (C=192: 6); wave w owns output channels [32w, 32w+32) of every
+// row of a BM=32-pixel tile.  Two blocks share a CU (72 KB LDS each, three
+// waves per SIMD), so one block's epilogue and copy-out overlap the other's
+// MFMAs.
+template <int C>
+constexpr int fwd_waves() { return 4; }
+
 template <int C, int BM>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, 2)
     gdn_fwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                          const float* __restrict__ beta, int inverse, float* __restrict__ y,
                          float* __restrict__ norm, uint32_t P) {
-  constexpr int NT = 256;
-  constexpr int NTW = C / 64;    // 16-wide n-tiles per wave
+  constexpr int NW = fwd_waves<C>();
+  constexpr int NT = 64 * NW;
+  constexpr int NTW = C / 16 / NW;  // 16-wide n-tiles per wave
   constexpr int KU = C / 16;     // groups of 4 k-steps
-  constexpr int MT = BM / 16;    // 16-row m-tiles per wave
+  constexpr int MT = BM / 16;    // 16-row m-tiles
   constexpr int TILE = BM * C;
   constexpr int NSTORE = 2 * (BM * C / 4 / NT);  // vector-memory ops of one copy-out
   __shared__ __attribute__((aligned(16))) float lds[3 * TILE];  // 2 x-buffers + norm staging
@@ -99,8 +105,7 @@ __global__ void __launch_bounds__(256, 1)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int nbase = w * (C / 4);
-  constexpr int mbase = 0;
+  const int nbase = w * (C / NW);
   const uint32_t ntiles = (P + BM - 1) / BM;
 
   // bfr[j][4u+v] = gamma[n = nbase+16j+li][k = 16u+4lq+v]
@@ -136,14 +141,21 @@ __global__ void __launch_bounds__(256, 1)
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[mt][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    // A fragments one k-group ahead (software pipeline); the scheduling
+    // barrier keeps the compiler from hoisting all KU groups' LDS reads
+    floatx4v a4[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) a4[mt] = *(const floatx4v*)(xs + (16 * mt + li) * C + ((lq ^ li) << 2));
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-      floatx4v a4[MT];
+      floatx4v an[MT];
+      if (u + 1 < KU) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        a4[mt] = *(const floatx4v*)(xs + (mbase + 16 * mt + li) * C + (((4 * u + lq) ^ li) << 2));
-        a4[mt] = a4[mt] * a4[mt];
+        for (int mt = 0; mt < MT; ++mt)
+          an[mt] = *(const floatx4v*)(xs + (16 * mt + li) * C + (((4 * (u + 1) + lq) ^ li) << 2));
       }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a4[mt] = a4[mt] * a4[mt];
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -151,6 +163,11 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
           for (int j = 0; j < NTW; ++j)
             acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[mt][v], bfr[j][4 * u + v], acc[mt][j], 0, 0, 0);
+      if (u + 1 < KU) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a4[mt] = an[mt];
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // every wave's x^2 reads are done before y overwrites x in place
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -163,7 +180,7 @@ __global__ void __launch_bounds__(256, 1)
         const int n = nbase + 16 * j + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int off = swz<C>(mbase + 16 * mt + 4 * lq + r, n);
+          const int off = swz<C>(16 * mt + 4 * lq + r, n);
           const float nv = acc[mt][j][r] + bet[j];
           const float xv = xs[off];
           xs[off] = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
@@ -383,15 +400,15 @@ __global__ void gdn_slab_reduce_kernel(const float* __restrict__ slab, int nb, i
   }
 }
 
-constexpr int FWD_BM = 64;
+constexpr int FWD_BM = 16;
 
 template <int C>
 int gdn_fwd_fused_launch(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm,
                          long long P, hipStream_t s) {
   const long long ntiles = (P + FWD_BM - 1) / FWD_BM;
-  long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
+  long long grid = ntiles < 512 ? ntiles : 512;  // two blocks per CU
   if (grid < 1) return IC_OK;
-  hipLaunchKernelGGL((gdn_fwd_fused_kernel<C, FWD_BM>), dim3((unsigned)grid), dim3(256), 0, s, x, gamma, beta,
+  hipLaunchKernelGGL((gdn_fwd_fused_kernel<C, FWD_BM>), dim3((unsigned)grid), dim3(64 * fwd_waves<C>()), 0, s, x, gamma, beta,
                      inverse, y, norm, (uint32_t)P);
   IC_CHECK_LAUNCH();
   return IC_OK;

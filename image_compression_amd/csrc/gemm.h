@@ -117,3 +117,16 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s);
+
+// image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
+bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout);
+int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H, int W,
+                  const float* wp, int Kp, const float* bias, int k, int stride, int pad, float* y, long long ys_n,
+                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s);
+bool edge_wgrad_ok(int C, int k, int stride, long long sw, const float* G, int CG, long long gs_c, long long gs_w,
+                   long long gs_h, long long gs_n, int Ho, int Wo);
+long long edge_units(int N, int Ho, int Wo);
+size_t edge_wgrad_ws(int CG, int Kc, long long units);
+int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
+                   int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,
+                   void* ws, hipStream_t s);

@@ -75,10 +75,15 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
   const int phase = zi / d.ksplit;
   const int split = zi - phase * d.ksplit;
   const IgPhase& P = d.ph[phase];
-  if ((int)blockIdx.x >= P.mtiles) return;
+  // XCD-aware tile order: block b runs on XCD b % 8, so give each XCD a
+  // contiguous range of m-tiles (neighbouring output rows share input rows,
+  // which then hit that XCD's L2 instead of HBM)
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
 
   const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = blockIdx.x * BM;
+  const uint32_t m0 = bx * BM;
   const int n0 = blockIdx.y * BN;
   const int nchunks = GEN ? (d.Kc >> 5) : P.T * (d.Cin >> 5);
   const int cb = split * d.kcps;
