@@ -58,11 +58,11 @@ __device__ __forceinline__ uint32_t ig_out_offset(const IgDesc& d, const IgPhase
   return img * (uint32_t)d.ys_n + oy * (uint32_t)d.ys_h + ox * (uint32_t)d.ys_w;
 }
 
-__device__ __forceinline__ float aop(int op, float v) {
-  return op == AOP_SQUARE ? v * v : (op == AOP_ABS ? fabsf(v) : v);
-}
+__device__ __attribute__((aligned(16))) float ig_zero_page[4];
 
-template <int BM, int BN, int WM, int WN, bool GEN>
+// SQ: square the A operand (GDN's x^2 on the non-fused GDN path); a template
+// parameter so the conv main loop carries no per-element operand switch
+template <int BM, int BN, int WM, int WN, bool GEN, bool SQ>
 __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
   constexpr int WAVES_N = BN / WN;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -123,10 +123,11 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
       const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);         \
       _Pragma("unroll") for (int p = 0; p < APASS; ++p) {                                         \
         const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;                                           \
-        floatx4v v = {0.f, 0.f, 0.f, 0.f};                                                        \
-        if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)                       \
-          v = *(const floatx4v*)(xg + (a_off[p] + toff));                                         \
-        if (d.a_op) { v[0] = aop(d.a_op, v[0]); v[1] = aop(d.a_op, v[1]); v[2] = aop(d.a_op, v[2]); v[3] = aop(d.a_op, v[3]); } \
+        /* branch-free gather: zero padding reads a zero page */                                  \
+        const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;           \
+        const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;                            \
+        floatx4v v = *(const floatx4v*)src;                                                       \
+        if constexpr (SQ) v = v * v;                                                              \
         ra[p] = v;                                                                                \
       }                                                                                           \
       const float* wb = P.wp + ((size_t)t * d.Npad + n0 + lrow) * d.Cin + cc * 32 + lc4 * 4;      \
@@ -143,8 +144,9 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
             const int dy = P.dy[t], dx = P.dx[t];                                                 \
             const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;                                       \
             if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)                   \
-              val = aop(d.a_op, xg[a_off[p] + (uint32_t)(dy * (int)xsh + dx * (int)xsw) +         \
-                                   (uint32_t)ci * (uint32_t)d.xs_c]);                             \
+              val = xg[a_off[p] + (uint32_t)(dy * (int)xsh + dx * (int)xsw) +                    \
+                       (uint32_t)ci * (uint32_t)d.xs_c];                                         \
+            if constexpr (SQ) val *= val;                                                         \
           }                                                                                       \
           v4[e] = val;                                                                            \
         }                                                                                         \
@@ -227,6 +229,33 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
     return;
   }
   const uint32_t ysc = (uint32_t)d.ys_c;
+  if (d.epi == EPI_NONE || d.epi == EPI_RELU) {
+    // plain conv epilogue: bias hoisted per column, optional ReLU
+    float bj[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + r;
+      nok[j] = n < d.Cout;
+      bj[j] = (d.bias && nok[j]) ? d.bias[n] : 0.f;
+    }
+    const bool relu = d.epi == EPI_RELU;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m >= M) continue;
+        float* yo = d.y + ig_out_offset(d, P, m);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = acc[i][j][reg] + bj[j];
+          if (relu) v = v > 0.f ? v : 0.f;
+          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 32 + r) * ysc] = v;
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -266,10 +295,14 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   int mt = 0;
   for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
   dim3 grid(mt, d.Npad / BN, d.nphase * d.ksplit);
-  if (d.generic)
-    hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
-  else
-    hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
+  const bool sq = d.a_op == AOP_SQUARE;
+  if (d.generic) {
+    if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
+  } else {
+    if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, d);
+  }
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
