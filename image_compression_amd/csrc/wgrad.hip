@@ -200,7 +200,12 @@ __global__ void __launch_bounds__(256, 2) wg_kernel(const WgDesc d) {
 // (past the split, outside the image = zero padding) read a zero page.
 __device__ __attribute__((aligned(16))) float wg_zero_page[4];
 
-template <int BM, int BN, int WM, int WN>
+// LDS image rows are k (pixel) major; odd rows have their 16-B chunks XOR 8
+// (a 32-float shift), so the two lane halves of a fragment read (rows k, k+1
+// at the same columns) hit different banks.  Applied on the DMA source.
+__device__ __forceinline__ int wg_swz(int k, int col) { return ((((col >> 2) ^ ((k & 1) << 3))) << 2) | (col & 3); }
+
+template <int BM, int BN, int WM, int WN, bool XSQ>
 __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
   constexpr int BK = 16;
   constexpr int WAVES_N = BN / WN;
@@ -236,7 +241,7 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
 #pragma unroll
     for (int q = 0; q < GPASS; ++q) {
       const int f = tid + 256 * q;
-      const int row = f / G4, c4 = f - (f / G4) * G4;
+      const int row = f / G4, c4 = (f - (f / G4) * G4) ^ ((row & 1) << 3);
       const uint32_t p = p0 + row;
       const int col = g0 + c4 * 4;
       const float* src = wg_zero_page;
@@ -253,7 +258,7 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
 #pragma unroll
     for (int q = 0; q < XPASS; ++q) {
       const int f = tid + 256 * q;
-      const int row = f / X4, c4 = f - (f / X4) * X4;
+      const int row = f / X4, c4 = (f - (f / X4) * X4) ^ ((row & 1) << 3);
       const uint32_t p = p0 + row;
       const int col = c0 + c4 * 4;
       const float* src = wg_zero_page;
@@ -288,17 +293,16 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
     if (p0 + BK < pe) stage(p0 + BK, buf ^ 1);
     const float* Gs = lds + buf * STAGE;
     const float* Xs = Gs + BK * BM;
-    const bool x_sq = d.x_op == AOP_SQUARE;
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s) {
       const int k = 2 * s + h;
       float a[TM], bb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = Gs[k * BM + wm * WM + i * 32 + r];
+      for (int i = 0; i < TM; ++i) a[i] = Gs[k * BM + wg_swz(k, wm * WM + i * 32 + r)];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const float v = Xs[k * BN + wn * WN + j * 32 + r];
-        bb[j] = x_sq ? v * v : v;
+        const float v = Xs[k * BN + wg_swz(k, wn * WN + j * 32 + r)];
+        bb[j] = XSQ ? v * v : v;
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -391,7 +395,10 @@ int wg_launch_t(const WgDesc& d, hipStream_t s) {
 template <int BM, int BN, int WM, int WN>
 int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
-  hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+  if (d.x_op == AOP_SQUARE)
+    hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
+  else
+    hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
