@@ -122,23 +122,37 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-step-only", action="store_true",
                     help="only warmup+timed steps (for rocprofv3 runs)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from a hipGraph (TrainStep; N > 1: one flat RCCL all-reduce "
+                         "after the replay) instead of eager launches (N > 1: DDP, 12 MB buckets "
+                         "overlapped with the backward).  Measured equal at N=1: the GPU, not the host, "
+                         "paces the launches.")
     args = ap.parse_args()
 
     from image_compression_amd import distributed as D
     from image_compression_amd import modelling
     rank, world, dev = D.setup()
     dist = world > 1
+    from image_compression_amd.step import TrainStep
     torch.manual_seed(0)
-    model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev)
+    model = modelling.build_model(_cfg()).to(dev).train()
     # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
+    if not args.graph:
+        model = D.wrap(model, dev)
 
-    def step():
-        model.zero_grad(set_to_none=True)
-        _, losses = model(x)
-        losses["total_loss"].backward()
-        return losses
+        def step():
+            model.zero_grad(set_to_none=True)
+            _, losses = model(x)
+            losses["total_loss"].backward()
+            return losses
+        mode = "eager, DDP 12 MB buckets" if dist else "eager"
+    else:
+        # fwd + loss + bwd captured once into a hipGraph and replayed; for N > 1
+        # the flat gradient is all-reduced (RCCL) after each replay
+        step = TrainStep(model, x, graph=True)
+        mode = "hipGraph" + (" + RCCL all-reduce of the flat gradient" if dist else "")
 
     for _ in range(args.warmup):
         losses = step()
@@ -176,7 +190,7 @@ def main():
                     "(reference init, seed 0); training noise from in-kernel Philox",
             "config": {"workload": "C2: psnr_256 (lambda=256, MSE, Laplacian conditional, 192/192 ch), "
                                    f"{args.size}x{args.size}, {args.batch} images/GPU, fwd+loss+bwd"
-                                   + (" + RCCL grad all-reduce (DDP, 12 MB buckets)" if dist else ""),
+                                   + (" + grad all-reduce" if dist else "") + f" [{mode}]",
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(step_tflops, 2),

@@ -71,6 +71,7 @@ SIGNATURES = {
     "ic_mse_fwd": (c_int, [c_void, c_void, c_ll, c_void, c_void, c_size, c_void]),
     "ic_mse_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
     "ic_uniform": (c_int, [c_void, c_ll, c_ull, c_ull, c_void]),
+    "ic_philox_advance": (c_int, [c_void, c_ull, c_void]),
     "ic_factorized_fwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),
     "ic_factorized_bwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_void, c_void, c_void, P(ICFactGrads), c_void]),
     "ic_conditional_fwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),

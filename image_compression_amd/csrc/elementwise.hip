@@ -171,6 +171,12 @@ __global__ void uniform_k(float* u, long long n, unsigned long long seed, unsign
 
 }  // namespace
 
+namespace {
+__global__ void philox_advance_k(unsigned long long* state, unsigned long long n) {
+  if (threadIdx.x == 0) state[1] += n;
+}
+}  // namespace
+
 extern "C" {
 
 int ic_device_sync_check(void* stream) {
@@ -260,6 +266,12 @@ int ic_sqdiff_bwd(const float* a, const float* b, const float* g, long long n, f
 }
 int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset, void* stream) {
   hipLaunchKernelGGL(uniform_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, u, n, seed, offset);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_philox_advance(unsigned long long* state, unsigned long long n, void* stream) {
+  hipLaunchKernelGGL(philox_advance_k, dim3(1), dim3(64), 0, (hipStream_t)stream, state, n);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }

@@ -132,7 +132,15 @@ __device__ __forceinline__ float mlp_bwd(const ChanParams& q, float v, const Act
 __device__ __forceinline__ float quant(float x, int mode, const float* u, long long i,
                                        unsigned long long seed, unsigned long long off) {
   if (mode == 1) return rintf(x);
-  const float uu = mode == 0 ? u[i] : philox_uniform(seed, off + (unsigned long long)i);
+  float uu;
+  if (mode == 0) {
+    uu = u[i];
+  } else if (mode == 3) {  // device-resident {seed, base} (graph-safe stream)
+    const unsigned long long* st = (const unsigned long long*)u;
+    uu = philox_uniform(st[0], st[1] + off + (unsigned long long)i);
+  } else {
+    uu = philox_uniform(seed, off + (unsigned long long)i);
+  }
   return x + (uu - 0.5f);
 }
 

@@ -423,11 +423,12 @@ class FactorizedFn(Function):
 
     @staticmethod
     def forward(ctx, z, mode, u, seed, offset, *params):
-        _lib.require_device(z, u, *params)
+        _lib.require_device(z, None if mode == 3 else u, *params)
         L = _L()
         C = z.shape[1]
         zl = _to_last(z)
-        ul = None if u is None else _to_last(u.to(z.dtype))
+        # mode 3: `u` is the device {seed, base} state of the Philox stream
+        ul = u if (u is None or mode == 3) else _to_last(u.to(z.dtype))
         q = torch.empty_like(zl)
         p = torch.empty_like(zl)
         prm = [t.contiguous() for t in params]
@@ -463,13 +464,13 @@ class ConditionalFn(Function):
 
     @staticmethod
     def forward(ctx, y, scale, mean, kind, mode, u, seed, offset):
-        _lib.require_device(y, scale, mean, u)
+        _lib.require_device(y, scale, mean, None if mode == 3 else u)
         L = _L()
         y = _dense(y)
         scale = _match(scale, y)
         if mean is not None:
             mean = _match(mean, y)
-        if u is not None:
+        if u is not None and mode != 3:  # mode 3: `u` is the Philox device state
             u = _match(u.to(y.dtype), y)
         q = torch.empty_like(y)
         p = torch.empty_like(y)
@@ -508,8 +509,8 @@ def factorized(z, params, train, u=None):
     elif u is not None:
         mode, seed, off = 0, 0, 0
     else:
-        mode = 2
-        seed, off = _noise.philox_stream(z.numel())
+        mode, seed = 3, 0
+        u, off = _noise.philox_stream(z.numel(), z.device)
     return FactorizedFn.apply(z, mode, u, seed, off, *params)
 
 
@@ -519,8 +520,8 @@ def conditional(y, scale, mean, kind, train, u=None):
     elif u is not None:
         mode, seed, off = 0, 0, 0
     else:
-        mode = 2
-        seed, off = _noise.philox_stream(y.numel())
+        mode, seed = 3, 0
+        u, off = _noise.philox_stream(y.numel(), y.device)
     return ConditionalFn.apply(y, scale, mean, kind, mode, u, seed, off)
 
 

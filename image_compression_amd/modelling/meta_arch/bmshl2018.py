@@ -6,6 +6,7 @@ forward(x) -> (x_tilde.detach(), losses) with losses =
 total_loss carries grad."""
 import torch.nn as nn
 
+from ... import noise as _noise
 from ...functional import AbsFn
 from ..blocks import (ENTROPY_MODEL_REGISTRY, AnalysisTransform, HyperpriorAnalysisTransform,
                       HyperpriorSynthesisTransform, SynthesisTransform)
@@ -32,6 +33,8 @@ class Compressor2018(nn.Module):
         self.loss_names = ["y_entropy", "z_entropy", "bpp"] + list(self.distortion_loss_fns.keys())
 
     def forward(self, x):
+        if self.training:
+            _noise.begin_step(x.device)  # fresh Philox counters for this step
         N, _, H, W = x.shape
         num_pixels = N * H * W
         y = self.analysis_transform(x)

@@ -4,9 +4,17 @@ The reference draws `torch.rand_like(x) - 0.5` inside forward
 (modelling/blocks/entropy_model.py:230 for z, :333 for y; call order
 meta_arch/bmshl2018.py:73,76).  Here the uniforms are generated inside the
 quantize kernels by a counter-based Philox4x32-10 stream, so no noise tensor is
-materialised in HBM.  The stream seed is drawn once from torch's default CPU
-generator (so `torch.manual_seed` makes runs reproducible) and the counter
-advances by the number of elements each call consumes.
+materialised in HBM.
+
+The stream state lives on the device: a 2-word tensor {seed, base} per device.
+Each draw in a step uses counters base + offset + i, where `offset` is a host
+counter of the elements drawn so far in the step; `begin_step()` (called at the
+top of every training forward) advances the device base by the previous
+step's total with a kernel (ic_philox_advance).  Because the advance is a
+kernel rather than a changed launch argument, a training step captured into a
+hipGraph (image_compression_amd.step) replays with fresh noise every time.
+The seed is drawn once from torch's default CPU generator (so
+`torch.manual_seed` makes runs reproducible).
 
 For bit-level parity with the reference, exact uniform draws can be injected:
 
@@ -21,32 +29,64 @@ import threading
 
 import torch
 
+from . import _lib
+
 _state = threading.local()
 
 
 def _st():
-    if not hasattr(_state, "seed"):
+    if not hasattr(_state, "dev"):
         _state.seed = None
-        _state.offset = 0
+        _state.dev = {}       # device -> int64[2] {seed, base} tensor
+        _state.offset = {}    # device -> counters drawn so far this step
         _state.queue = []
     return _state
 
 
-def philox_stream(n):
-    """Reserve n counters; returns (seed, offset)."""
+def _key(device):
+    d = torch.device(device)
+    return (d.type, d.index if d.index is not None else torch.cuda.current_device())
+
+
+def device_state(device):
+    """The {seed, base} tensor of `device` (created on first use)."""
     s = _st()
-    if s.seed is None:
-        s.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        s.offset = 0
-    off = s.offset
-    s.offset += int(n)
-    return s.seed, off
+    k = _key(device)
+    if k not in s.dev:
+        if s.seed is None:
+            s.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        s.dev[k] = torch.tensor([s.seed, 0], dtype=torch.int64, device=torch.device(*k))
+        s.offset[k] = 0
+    return s.dev[k]
+
+
+def philox_stream(n, device):
+    """Reserve n counters of this step; returns (state tensor, offset)."""
+    s = _st()
+    st = device_state(device)
+    k = _key(device)
+    off = s.offset[k]
+    s.offset[k] = off + int(n)
+    return st, off
+
+
+def begin_step(device):
+    """Advance the device base past the counters the previous step drew."""
+    s = _st()
+    k = _key(device)
+    n = s.offset.get(k, 0)
+    if n:
+        _lib.check(_lib.load().ic_philox_advance(_lib.ptr(s.dev[k]), _lib.c_ull(n),
+                                                 _lib.c_void(torch.cuda.current_stream(s.dev[k].device).cuda_stream)),
+                   "philox_advance")
+        s.offset[k] = 0
 
 
 def reseed(seed=None):
     s = _st()
     s.seed = None if seed is None else int(seed)
-    s.offset = 0
+    s.dev = {}
+    s.offset = {}
 
 
 def pop_injected():

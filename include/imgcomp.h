@@ -126,12 +126,19 @@ int ic_mse_bwd(const float* a, const float* b, const float* gout, long long n, f
 /* ---- noise: u[i] = Philox4x32-10(seed, offset + i) -> U[0,1) ---- */
 int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset,
                void* stream);
+/* graph-safe noise stream: a device-resident state {seed, base}; quantizers in
+ * mode 3 draw Philox(seed, base + offset + i).  Advancing the base by the
+ * counters one training step consumed is itself a kernel, so a captured
+ * hipGraph replays with fresh noise every time.  state[1] += n */
+int ic_philox_advance(unsigned long long* state, unsigned long long n, void* stream);
 
 /* ---- factorized entropy model (z): C channels, elements e with channel c = idx % C
  *      (channels-last storage). params (device, fp32, reference shapes flattened):
  *      w0[C*3] b0[C*3] f0[C*3] w1[C*9] b1[C*3] f1[C*3] w2[C*9] b2[C*3] f2[C*3] w3[C*3] b3[C]
  *      mode: 0 = noise with given u (u in [0,1), y = z + (u - 0.5)), 1 = round,
- *            2 = noise from Philox(seed, offset) */
+ *            2 = noise from Philox(seed, offset),
+ *            3 = noise from Philox(state[0], state[1] + offset) with `u` pointing to the
+ *                device state {seed, base} of ic_philox_advance (`seed` ignored) */
 typedef struct ic_fact_params {
   const float *w0, *b0, *f0, *w1, *b1, *f1, *w2, *b2, *f2, *w3, *b3;
 } ic_fact_params;
@@ -148,7 +155,8 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
                       void* stream);
 
 /* ---- conditional (Laplacian kind=0 / Gaussian kind=1), mean = 0 or tensor ----
- *      q = y + (u - 0.5) (mode 0), round(y) (mode 1), Philox (mode 2)
+ *      q = y + (u - 0.5) (mode 0), round(y) (mode 1), Philox (mode 2), Philox on the
+ *      device state `u` (mode 3, as for ic_factorized_fwd)
  *      p = F((0.5-|q-mean|)/scale) - F((-0.5-|q-mean|)/scale) */
 int ic_conditional_fwd(const float* y, const float* scale, const float* mean, long long n, int kind,
                        int mode, const float* u, unsigned long long seed,
