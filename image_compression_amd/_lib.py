@@ -32,6 +32,11 @@ class ICFactGrads(ctypes.Structure):
     _fields_ = [(f, c_void) for f in _FACT_FIELDS]
 
 
+class ICAdamWTensor(ctypes.Structure):
+    _fields_ = [("param", c_void), ("grad", c_void), ("exp_avg", c_void), ("exp_avg_sq", c_void),
+                ("n", c_ll), ("lr", c_float), ("weight_decay", c_float)]
+
+
 P = ctypes.POINTER
 _ACT = P(ICAct)
 
@@ -72,6 +77,8 @@ SIGNATURES = {
     "ic_mse_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
     "ic_uniform": (c_int, [c_void, c_ll, c_ull, c_ull, c_void]),
     "ic_philox_advance": (c_int, [c_void, c_ull, c_void]),
+    "ic_adamw_step": (c_int, [P(ICAdamWTensor), c_int, ctypes.c_double, ctypes.c_double, c_float, c_float, c_ll,
+                              c_void]),
     "ic_factorized_fwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),
     "ic_factorized_bwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_void, c_void, c_void, P(ICFactGrads), c_void]),
     "ic_conditional_fwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),

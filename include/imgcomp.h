@@ -33,6 +33,8 @@
  *   ce_loss_*           modelling/blocks/entropy_model.py:171-185 (_ce_loss)
  *   mse_*, sqdiff_*     nn.MSELoss(reduction="mean"/"none") in modelling/loss.py:25
  *   msssim_*            modelling/loss.py:48-188 (SSIMLoss, MS_SSIMLoss)
+ *   adamw_step          torch.optim.AdamW of solver/optim.py:20-45 + clip_grad_value_ of
+ *                       engine/trainer.py:189-190 (the training step around the path)
  */
 #ifndef IMGCOMP_H
 #define IMGCOMP_H
@@ -164,6 +166,24 @@ int ic_conditional_fwd(const float* y, const float* scale, const float* mean, lo
 int ic_conditional_bwd(const float* q, const float* scale, const float* mean, long long n, int kind,
                        const float* dq, const float* dp, float* dy, float* dscale, float* dmean,
                        void* stream);
+
+/* ---- optimizer: multi-tensor AdamW with fused clip_grad_value_ ----
+ * torch.optim.AdamW (solver/optim.py:20-45: per-parameter lr / weight_decay
+ * groups) preceded by clip_grad_value_(clip) (engine/trainer.py:189-190; clip
+ * <= 0 disables it; clipped gradients are written back).  `step` is the
+ * 1-based step count used for the bias corrections (betas in double, like the
+ * reference's Python floats).  All pointers device fp32. */
+typedef struct ic_adamw_tensor {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long n;
+  float lr;
+  float weight_decay;
+} ic_adamw_tensor;
+int ic_adamw_step(const ic_adamw_tensor* tensors, int ntensors, double beta1, double beta2, float eps,
+                  float clip, long long step, void* stream);
 
 /* ---- SSIM / MS-SSIM (modelling/loss.py:48-188) on [N][C][H][W] contiguous images in [0,1].
  *      nlev levels (MS-SSIM: 5, weights[nlev] host array; single=1 for SSIMLoss, nlev=1).
