@@ -77,6 +77,9 @@ SIGNATURES = {
     "ic_mse_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
     "ic_uniform": (c_int, [c_void, c_ll, c_ull, c_ull, c_void]),
     "ic_philox_advance": (c_int, [c_void, c_ull, c_void]),
+    "ic_psnr": (c_int, [c_void, c_void, c_int, c_ll, c_float, c_void, c_void]),
+    "ic_images_u8_to_input": (c_int, [c_void, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void, c_void, c_void,
+                                      c_void]),
     "ic_adamw_step": (c_int, [P(ICAdamWTensor), c_int, ctypes.c_double, ctypes.c_double, c_float, c_float, c_ll,
                               c_void]),
     "ic_factorized_fwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),

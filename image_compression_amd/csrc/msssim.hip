@@ -210,13 +210,14 @@ __global__ void combine_k(const float* stats, const Comb cb, float* out) {
       cs = fmaxf(cs, e); ss = fmaxf(ss, e);
       const float t = (l < cb.nlev - 1) ? cs : ss;
       if (cb.log_scale) v += logf(t) * cb.w[l];
-      else v *= (cb.single ? t : powf(t, cb.w[l]));
+      else v *= (cb.single == 1 ? t : powf(t, cb.w[l]));
     }
-    if (cb.single && cb.log_scale) out[n] = -v;
+    if (cb.single == 2) out[n] = -10.f * logf(1.f - v) / 2.302585092994046f;  // metric, dB per image
+    else if (cb.single && cb.log_scale) out[n] = -v;
     else vals[n] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0 && !(cb.single && cb.log_scale)) {
+  if (threadIdx.x == 0 && cb.single != 2 && !(cb.single && cb.log_scale)) {
     float s = 0;
     for (int n = 0; n < cb.N; ++n) s += vals[n];
     const float m = s / (float)cb.N;

@@ -188,6 +188,9 @@ int ic_adamw_step(const ic_adamw_tensor* tensors, int ntensors, double beta1, do
 /* ---- SSIM / MS-SSIM (modelling/loss.py:48-188) on [N][C][H][W] contiguous images in [0,1].
  *      nlev levels (MS-SSIM: 5, weights[nlev] host array; single=1 for SSIMLoss, nlev=1).
  *      out: log_scale && single -> out[N] = -log(max(ssim_n, eps)); else out[0] = loss.
+ *      single = 2 (with log_scale = 0, eps = 0): the evaluation metric of
+ *      utils/metric.py:100-124 — out[N] = -10 log10(1 - prod_l max(cs_l,0)^w_l * max(ssim,0)^w_L)
+ *      per image (MS_SSIM(in_dB=True), images scaled by max_val); forward only.
  *      `state` (ic_msssim_state_bytes) is written by fwd and read by bwd. */
 size_t ic_msssim_state_bytes(int N, int C, int H, int W, int nlev, int filter_size);
 size_t ic_msssim_ws(int N, int C, int H, int W, int nlev, int filter_size);
@@ -199,6 +202,16 @@ int ic_msssim_bwd(int N, int C, int H, int W, int nlev, int filter_size, float f
                   float max_val, int log_scale, int single, float k1, float k2, float eps,
                   const float* weights, const float* gout, const float* state, float* ga, float* gb,
                   void* ws, size_t ws_bytes, void* stream);
+
+/* ---- evaluation metric: per-image PSNR in dB (utils/metric.py:26-36) of images scaled by
+ *      max_val: out[n] = 10 (2 log10(max_val) - log(mse_n) / ln 10), a, b [N][per_image] ---- */
+int ic_psnr(const float* a, const float* b, int N, long long per_image, float max_val, float* out, void* stream);
+
+/* ---- host data path: uint8 HWC images (byte strides sn, sh, sw; channel stride 1) -> fp32
+ *      NCHW model input (x/255 - mean[c]) / std[c] (transforms.py ToTensor, ChannelFirst,
+ *      Normalize; mean/std host arrays of C <= 3 values or NULL for 0 / 1) ---- */
+int ic_images_u8_to_input(const unsigned char* x, long long sn, long long sh, long long sw, int N, int C, int H,
+                          int W, const float* mean, const float* std, float* y, void* stream);
 
 /* ---- elementwise squared difference (MSE with reduction="none") ---- */
 int ic_sqdiff_fwd(const float* a, const float* b, long long n, float* out, void* stream);

@@ -305,6 +305,35 @@ def ssim_loss(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
     return 1.0 - ssim.mean()
 
 
+# ---------------------------------------------------------------- eval metrics
+def psnr_metric(a, b, max_val=255.0):
+    """utils/metric.py:26-36 on images already scaled by 255 (the Monitor
+    multiplies x, x~ by 255 first, engine/monitor.py:118-121): per-image
+    10 * (2 log10(max) - log(mse)/ln 10), mse over (C, H, W)."""
+    m = F.mse_loss(a, b, reduction="none").mean((1, 2, 3))
+    return 10.0 * (2 * math.log10(max_val) - m.log() / math.log(10))
+
+
+def ms_ssim_metric_db(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
+                      weights=(0.0448, 0.2856, 0.3001, 0.2363, 0.1333)):
+    """utils/metric.py:100-138 MS_SSIM(in_dB=True) on images already scaled by
+    255: per-image prod_l max(cs_l, 0)^w_l * max(ssim_L, 0)^w_L (SSIM with
+    non_negative=True, metric.py:39-72), then -10 log10(1 - result)."""
+    filt = _gauss_filter2d(size, sigma, a.dtype)
+    c1, c2 = (k1 * max_val) ** 2, (k2 * max_val) ** 2
+    res = torch.ones((a.shape[0],), dtype=a.dtype)
+    n = len(weights)
+    for i, w in enumerate(weights, 1):
+        ssim, cs = _ssim_terms(a, b, filt, c1, c2, 0.0, False)
+        ssim, cs = torch.clamp_min(ssim, 0.0), torch.clamp_min(cs, 0.0)
+        if i < n:
+            res = res * cs ** w
+            a, b = _downsample(a), _downsample(b)
+        else:
+            res = res * ssim ** w
+    return -10.0 * (1.0 - res).log() / math.log(10)
+
+
 # ---------------------------------------------------------------- full model
 def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             loss_names=("MSE",), lam=256.0, ssim_log=True,

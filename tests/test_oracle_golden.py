@@ -4,7 +4,9 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (assert_close, golden_names, load_golden, oracle_kwargs,
+import os
+
+from conftest import (GOLDEN, assert_close, golden_names, load_golden, oracle_kwargs,
                       params_of, rel_err)
 from oracle import ref_cpu
 
@@ -51,3 +53,16 @@ def test_gdn_known_answers():
     xr = torch.clamp(x, min=0)
     exp = xr / torch.sqrt(1 + 0.1 * xr ** 2)
     assert (ref_cpu.gdn(x, gp, bp, relu=True) - exp).abs().max() <= 1e-6
+
+
+def test_oracle_eval_metrics_match_reference():
+    """oracle/ref_cpu.py psnr_metric / ms_ssim_metric_db vs the reference's
+    utils/metric.py (tests/golden/eval_metrics.npz)."""
+    import torch
+    from test_eval import _metric_inputs
+    gold = np.load(os.path.join(GOLDEN, "eval_metrics.npz"))
+    for name, (x, xt) in _metric_inputs().items():
+        p = ref_cpu.psnr_metric(xt * 255.0, x * 255.0).numpy()
+        m = ref_cpu.ms_ssim_metric_db(xt * 255.0, x * 255.0).numpy()
+        assert np.abs(p - gold[f"{name}_psnr"]).max() < 1e-4
+        assert np.abs(m - gold[f"{name}_msssim_db"]).max() < 1e-4
