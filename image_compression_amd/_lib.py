@@ -44,6 +44,17 @@ _ACT = P(ICAct)
 SIGNATURES = {
     "ic_version": (c_int, []),
     "ic_device_sync_check": (c_int, [c_void]),
+    "ic_conv2d_fwd_ws_ex": (c_size, [_ACT, c_int, c_int, c_int, _ACT, c_int]),
+    "ic_conv2d_fwd_ex": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int, c_void, c_size,
+                                 c_void]),
+    "ic_conv2d_dgrad_ws_ex": (c_size, [_ACT, c_int, c_int, c_int, _ACT, c_int]),
+    "ic_conv2d_dgrad_ex": (c_int, [_ACT, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size, c_void]),
+    "ic_conv_transpose2d_fwd_ws_ex": (c_size, [_ACT, c_int, c_int, c_int, _ACT, c_int]),
+    "ic_conv_transpose2d_fwd_ex": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int, c_void,
+                                           c_size, c_void]),
+    "ic_conv_transpose2d_dgrad_ws_ex": (c_size, [_ACT, c_int, c_int, c_int, _ACT, c_int]),
+    "ic_conv_transpose2d_dgrad_ex": (c_int, [_ACT, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size,
+                                             c_void]),
     "ic_conv2d_fwd_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),
     "ic_conv2d_fwd": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size, c_void]),
     "ic_conv2d_dgrad_ws": (c_size, [_ACT, c_int, c_int, c_int, _ACT]),

@@ -135,7 +135,8 @@ int transposed_col2im(const ic_act* x, const float* W, const float* bias, int k,
 // y[a] = sum_{t,b} x[b] @ (gy*s + ky - pad) * W[a][b][ky][kx]   (W: [A=y->c][B=x->c][k][k])
 int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
                 const ic_act* y, int epi, int aop, const float* aux0, const float* aux1,
-                const float* aux2, float* aux_out, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+                const float* aux2, float* aux_out, void* ws, size_t wsb, hipStream_t s, size_t* need,
+                int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
   if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w)
@@ -159,8 +160,10 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   }
   P.Hg = y->h; P.Wg = y->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;
   d.Kc = d.generic ? (int)ic_align((size_t)P.T * x->c, 32) : x->c;
+  d.bf16 = (math & IC_MATH_BF16) && !d.generic && x->c % 64 == 0 && aop == AOP_NONE;
   const size_t part = ig_plan(d);
-  const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * 4;
+  const size_t esz = d.bf16 ? 2 : 4;
+  const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * esz;
   const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
   if (need) { *need = tot; return IC_OK; }
   if (wsb < tot) return IC_ERR_WORKSPACE;
@@ -168,14 +171,14 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   float* wp = cv.take(wpb);
   d.partial = part ? cv.take(part) : nullptr;
   P.wp = wp;
-  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s);
+  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.bf16);
   if (rc) return rc;
   return ig_run(d, s);
 }
 
 // y[b] at (s*iy - pad + ky) += x[a] @ iy * W[a][b][ky][kx]    (W: [A=x->c][B=y->c][k][k])
 int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
-                    const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+                    const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1 || stride > 2) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
   if ((y->h + 2 * pad - k) / stride + 1 != x->h || (y->w + 2 * pad - k) / stride + 1 != x->w)
@@ -216,11 +219,12 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
     }
   d.nphase = np;
   d.Kc = d.generic ? (int)ic_align((size_t)tmax * x->c, 32) : x->c;
+  d.bf16 = (math & IC_MATH_BF16) && !d.generic && x->c % 64 == 0;
   const size_t part = ig_plan(d);
   size_t wpb[IC_MAXPH];
   size_t tot = ic_align(part, 256);
   for (int p = 0; p < np; ++p) {
-    wpb[p] = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)d.ph[p].T * d.Npad * x->c * 4;
+    wpb[p] = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)d.ph[p].T * d.Npad * x->c * (d.bf16 ? 2 : 4);
     tot += ic_align(wpb[p], 256);
   }
   if (need) { *need = tot; return IC_OK; }
@@ -230,7 +234,7 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   for (int p = 0; p < np; ++p) {
     float* wp = cv.take(wpb[p]);
     d.ph[p].wp = wp;
-    int rc = pack_weights(W, x->c, y->c, k, 1, d.generic, d.ph[p].T, pky[p], pkx[p], d.Npad, d.Kc, wp, s);
+    int rc = pack_weights(W, x->c, y->c, k, 1, d.generic, d.ph[p].T, pky[p], pkx[p], d.Npad, d.Kc, wp, s, d.bf16);
     if (rc) return rc;
   }
   return ig_run(d, s);
@@ -324,28 +328,42 @@ extern "C" {
 
 int ic_version(void) { return 1; }
 
-size_t ic_conv2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math) {
   size_t n = 0;
   int rc = direct_impl(x, nullptr, nullptr, k, stride, pad, y, EPI_NONE, AOP_NONE, nullptr, nullptr,
-                       nullptr, nullptr, nullptr, 0, 0, &n);
+                       nullptr, nullptr, nullptr, 0, 0, &n, math);
   return need_or_zero(rc, n);
+}
+int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                     const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream) {
+  return direct_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, AOP_NONE, nullptr,
+                     nullptr, nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
+}
+size_t ic_conv2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+  return ic_conv2d_fwd_ws_ex(x, k, stride, pad, y, 0);
 }
 int ic_conv2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
                   const ic_act* y, int act, void* ws, size_t ws_bytes, void* stream) {
-  return direct_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, AOP_NONE, nullptr,
-                     nullptr, nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr);
+  return ic_conv2d_fwd_ex(x, w, b, k, stride, pad, y, act, 0, ws, ws_bytes, stream);
 }
 
-size_t ic_conv2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+size_t ic_conv2d_dgrad_ws_ex(const ic_act* dy, int k, int stride, int pad, const ic_act* dx, int math) {
   size_t n = 0;
-  int rc = transposed_impl(dy, nullptr, nullptr, k, stride, pad, dx, EPI_NONE, nullptr, 0, 0, &n);
+  int rc = transposed_impl(dy, nullptr, nullptr, k, stride, pad, dx, EPI_NONE, nullptr, 0, 0, &n, math);
   return need_or_zero(rc, n);
+}
+int ic_conv2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx, int math,
+                       void* ws, size_t ws_bytes, void* stream) {
+  // conv weight [Cout][Cin] is the transposed-gather weight [A=Cout (dy ch)][B=Cin (dx ch)]
+  return transposed_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, ws, ws_bytes,
+                         (hipStream_t)stream, nullptr, math);
+}
+size_t ic_conv2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+  return ic_conv2d_dgrad_ws_ex(dy, k, stride, pad, dx, 0);
 }
 int ic_conv2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx,
                     void* ws, size_t ws_bytes, void* stream) {
-  // conv weight [Cout][Cin] is the transposed-gather weight [A=Cout (dy ch)][B=Cin (dx ch)]
-  return transposed_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, ws, ws_bytes,
-                         (hipStream_t)stream, nullptr);
+  return ic_conv2d_dgrad_ex(dy, w, k, stride, pad, dx, 0, ws, ws_bytes, stream);
 }
 
 size_t ic_conv2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {
@@ -358,29 +376,43 @@ int ic_conv2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pa
   return wgrad_impl(dy, x, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr);
 }
 
-size_t ic_conv_transpose2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+size_t ic_conv_transpose2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math) {
   size_t n = 0;
-  int rc = transposed_impl(x, nullptr, nullptr, k, stride, pad, y, EPI_NONE, nullptr, 0, 0, &n);
+  int rc = transposed_impl(x, nullptr, nullptr, k, stride, pad, y, EPI_NONE, nullptr, 0, 0, &n, math);
   return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                               const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream) {
+  return transposed_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, ws, ws_bytes,
+                         (hipStream_t)stream, nullptr, math);
+}
+size_t ic_conv_transpose2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
+  return ic_conv_transpose2d_fwd_ws_ex(x, k, stride, pad, y, 0);
 }
 int ic_conv_transpose2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride,
                             int pad, const ic_act* y, int act, void* ws, size_t ws_bytes,
                             void* stream) {
-  return transposed_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, ws, ws_bytes,
-                         (hipStream_t)stream, nullptr);
+  return ic_conv_transpose2d_fwd_ex(x, w, b, k, stride, pad, y, act, 0, ws, ws_bytes, stream);
 }
 
-size_t ic_conv_transpose2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+size_t ic_conv_transpose2d_dgrad_ws_ex(const ic_act* dy, int k, int stride, int pad, const ic_act* dx, int math) {
   size_t n = 0;
   int rc = direct_impl(dy, nullptr, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
-                       nullptr, nullptr, nullptr, 0, 0, &n);
+                       nullptr, nullptr, nullptr, 0, 0, &n, math);
   return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx,
+                                 int math, void* ws, size_t ws_bytes, void* stream) {
+  // tconv weight [Cin][Cout] is the direct-gather weight [A=Cin (dx ch)][B=Cout (dy ch)]
+  return direct_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
+                     nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
+}
+size_t ic_conv_transpose2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
+  return ic_conv_transpose2d_dgrad_ws_ex(dy, k, stride, pad, dx, 0);
 }
 int ic_conv_transpose2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad,
                               const ic_act* dx, void* ws, size_t ws_bytes, void* stream) {
-  // tconv weight [Cin][Cout] is the direct-gather weight [A=Cin (dx ch)][B=Cout (dy ch)]
-  return direct_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
-                     nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr);
+  return ic_conv_transpose2d_dgrad_ex(dy, w, k, stride, pad, dx, 0, ws, ws_bytes, stream);
 }
 
 size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {

@@ -53,6 +53,7 @@ struct IgDesc {
   float* partial;    // [ksplit][Mtot][Cout]
   long long Mtot;
   int bm, bn;        // chosen tile (set by ig_plan)
+  int bf16;          // bf16 operands, fp32 accumulation (fast path, Cin % 64 == 0); wp holds bf16
   IgPhase ph[IC_MAXPH];
 };
 
@@ -100,7 +101,7 @@ int colsum(const float* t, long long s_n, long long s_c, long long s_h, long lon
 //  mode 2 (scatter):    wp[0][t*B + b][a] = W[a][b][ky_t][kx_t]   (rows n >= T*B zero)
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic,
                  int T, const int* ky, const int* kx, int Npad, int Kpad,
-                 float* wp, hipStream_t s);
+                 float* wp, hipStream_t s, int out_bf16 = 0);  // out_bf16: wp is __bf16[]
 
 // few-channel edges (im2col.hip)
 int im2col_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H,

@@ -58,6 +58,71 @@ __device__ __forceinline__ uint32_t ig_out_offset(const IgDesc& d, const IgPhase
   return img * (uint32_t)d.ys_n + oy * (uint32_t)d.ys_h + ox * (uint32_t)d.ys_w;
 }
 
+// epilogue shared by the fp32 and bf16 kernels.  C/D map of the 32x32 MFMA:
+// col = lane&31, row = (reg&3)+8*(reg>>2)+4*(lane>>5)
+template <int TM, int TN>
+__device__ __forceinline__ void ig_epilogue(const IgDesc& d, const IgPhase& P, floatx16 (&acc)[TM][TN], uint32_t M,
+                                            uint32_t m0, int n0, int wm, int wn, int WM, int WN, int r, int h,
+                                            int split) {
+  if (d.ksplit > 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m >= M) continue;
+        float* prow = d.partial + ((size_t)split * d.Mtot + P.m_off + m) * d.Cout;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WN + j * 32 + r;
+          if (n < d.Cout) prow[n] = acc[i][j][reg];
+        }
+      }
+    return;
+  }
+  const uint32_t ysc = (uint32_t)d.ys_c;
+  if (d.epi == EPI_NONE || d.epi == EPI_RELU) {
+    // plain conv epilogue: bias hoisted per column, optional ReLU
+    float bj[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + r;
+      nok[j] = n < d.Cout;
+      bj[j] = (d.bias && nok[j]) ? d.bias[n] : 0.f;
+    }
+    const bool relu = d.epi == EPI_RELU;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (m >= M) continue;
+        float* yo = d.y + ig_out_offset(d, P, m);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = acc[i][j][reg] + bj[j];
+          if (relu) v = v > 0.f ? v : 0.f;
+          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 32 + r) * ysc] = v;
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (m >= M) continue;
+      const uint32_t ob = ig_out_offset(d, P, m);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 32 + r;
+        if (n < d.Cout) ig_store_out(d, acc[i][j][reg], ob + (uint32_t)n * ysc, n);
+      }
+    }
+}
+
 __device__ __attribute__((aligned(16))) float ig_zero_page[4];
 
 // SQ: square the A operand (GDN's x^2 on the non-fused GDN path); a template
@@ -211,64 +276,133 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
 #undef IG_GLOAD
 #undef IG_SSTORE
 
-  // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (reg&3)+8*(reg>>2)+4*(lane>>5)
-  if (d.ksplit > 1) {
+  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
+}
+
+// ------------------------------------------------------------------ bf16
+// Same implicit GEMM with bf16 operands and fp32 accumulation
+// (v_mfma_f32_32x32x16_bf16): activations are read as fp32 and rounded to
+// bf16 (round-to-nearest-even, v_cvt_pk_bf16_f32) on their way into LDS,
+// weights come pre-packed in bf16.  K chunk = 64 channels of one tap
+// (Cin % 64 == 0); LDS rows of 72 bf16 (144 B) make the 16-row fragment
+// reads bank-conflict-free.  One MFMA consumes 16 k: lane (r, h) holds
+// A[row r][k 8h..8h+7] and B[k 8h..8h+7][col r].
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
+  constexpr int LDKB = 72;
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int APASS = BM / 16, BPASS = BN / 32;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LDKB];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * LDKB];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int n0 = blockIdx.y * BN;
+  const int cpt = d.Cin >> 6;
+  const int nchunks = P.T * cpt;
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x;
+  const int arow = tid >> 4, ac4 = tid & 15;   // A: 16 float4 per 64-wide row
+  const int brow = tid >> 3, bc8 = tid & 7;    // B: 8 x 16 B per 64-wide bf16 row
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[APASS];
+  int a_iy[APASS], a_ix[APASS];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (m >= M) continue;
-        float* prow = d.partial + ((size_t)split * d.Mtot + P.m_off + m) * d.Cout;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wn * WN + j * 32 + r;
-          if (n < d.Cout) prow[n] = acc[i][j][reg];
-        }
-      }
-    return;
+  for (int p = 0; p < APASS; ++p) {
+    const uint32_t m = m0 + arow + 16 * p;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[p] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[p] = (int)gx * d.stride;
+    a_off[p] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[p] * xsh + (uint32_t)a_ix[p] * xsw;
   }
-  const uint32_t ysc = (uint32_t)d.ys_c;
-  if (d.epi == EPI_NONE || d.epi == EPI_RELU) {
-    // plain conv epilogue: bias hoisted per column, optional ReLU
-    float bj[TN];
-    bool nok[TN];
+  const float* __restrict__ xg = d.x;
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+
+  floatx4v ra[APASS];
+  bf16x8 rb[BPASS];
+  auto gload = [&](int c) {
+    const int t = c / cpt, cc = c - t * cpt;
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 64 + ac4 * 4);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 32 + r;
-      nok[j] = n < d.Cout;
-      bj[j] = (d.bias && nok[j]) ? d.bias[n] : 0.f;
+    for (int p = 0; p < APASS; ++p) {
+      const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;
+      ra[p] = *(const floatx4v*)src;
     }
-    const bool relu = d.epi == EPI_RELU;
+    const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 64 + bc8 * 8;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int p = 0; p < BPASS; ++p) rb[p] = *(const bf16x8*)(wb + (size_t)(32 * p) * d.Cin);
+  };
+  auto sstore = [&]() {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (m >= M) continue;
-        float* yo = d.y + ig_out_offset(d, P, m);
+    for (int p = 0; p < APASS; ++p) {
+      bf16x4 v;
+      v[0] = (__bf16)ra[p][0]; v[1] = (__bf16)ra[p][1]; v[2] = (__bf16)ra[p][2]; v[3] = (__bf16)ra[p][3];
+      *(bf16x4*)&As[(arow + 16 * p) * LDKB + ac4 * 4] = v;
+    }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float v = acc[i][j][reg] + bj[j];
-          if (relu) v = v > 0.f ? v : 0.f;
-          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 32 + r) * ysc] = v;
-        }
-      }
-    return;
-  }
+    for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[(brow + 32 * p) * LDKB + bc8 * 8] = rb[p];
+  };
+
+  const int lane = tid & 63, w = tid >> 6;
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 31, h = lane >> 5;
+  floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (m >= M) continue;
-      const uint32_t ob = ig_out_offset(d, P, m);
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WN + j * 32 + r;
-        if (n < d.Cout) ig_store_out(d, acc[i][j][reg], ob + (uint32_t)n * ysc, n);
-      }
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (cb < ce) {
+    gload(cb);
+    sstore();
+  }
+  __syncthreads();
+  const __bf16* Ard = &As[(wm * WM + r) * LDKB + 8 * h];
+  const __bf16* Brd = &Bs[(wn * WN + r) * LDKB + 8 * h];
+  for (int c = cb; c < ce; ++c) {
+    if (c + 1 < ce) gload(c + 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const bf16x8*)(Ard + i * 32 * LDKB + 16 * s);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const bf16x8*)(Brd + j * 32 * LDKB + 16 * s);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    __syncthreads();
+    if (c + 1 < ce) sstore();
+    __syncthreads();
+  }
+  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
 }
 
 // split-K reduction + epilogue: one thread per (row, channel)
@@ -296,7 +430,10 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
   dim3 grid(mt, d.Npad / BN, d.nphase * d.ksplit);
   const bool sq = d.a_op == AOP_SQUARE;
-  if (d.generic) {
+  if (d.bf16) {
+    if (sq) return IC_ERR_ARG;
+    hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+  } else if (d.generic) {
     if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
   } else {
@@ -332,7 +469,7 @@ size_t ig_plan(IgDesc& d) {
     P.m_off = mtot;
     mtot += M;
     tiles += (long long)P.mtiles * (d.Npad / d.bn);
-    const int nch = d.generic ? (d.Kc >> 5) : P.T * (d.Cin >> 5);
+    const int nch = d.generic ? (d.Kc >> 5) : P.T * (d.bf16 ? (d.Cin >> 6) : (d.Cin >> 5));
     nchunks_max = nch > nchunks_max ? nch : nchunks_max;
   }
   d.Mtot = mtot;
@@ -357,6 +494,7 @@ size_t ig_plan(IgDesc& d) {
 int ig_run(IgDesc& d, hipStream_t s) {
   if (d.Mtot == 0) return IC_OK;
   if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
+  if (d.bf16 && (d.generic || d.Cin % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
   if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);

@@ -10,6 +10,7 @@ namespace {
 struct PackArgs {
   const float* W;
   float* wp;
+  int out_bf16;
   int A, B, k, mode, generic, T, Npad, Kpad;
   int ky[IC_MAXT], kx[IC_MAXT];
 };
@@ -40,7 +41,8 @@ __global__ void pack_kernel(const PackArgs p) {
       const int nn = (int)(i / p.A);
       const int tt = nn / p.B, b = nn - (nn / p.B) * p.B;
       if (tt < p.T) v = p.W[(((long long)a * p.B + b) * p.k + p.ky[tt]) * p.k + p.kx[tt]];
-      p.wp[i] = v;
+      if (p.out_bf16) ((__bf16*)p.wp)[i] = (__bf16)v;
+      else p.wp[i] = v;
       continue;
     }
     if (n < Nout && t < p.T) {
@@ -48,16 +50,17 @@ __global__ void pack_kernel(const PackArgs p) {
       const int b = p.mode == 0 ? r : n;
       v = p.W[(((long long)a * p.B + b) * p.k + p.ky[t]) * p.k + p.kx[t]];
     }
-    p.wp[i] = v;
+    if (p.out_bf16) ((__bf16*)p.wp)[i] = (__bf16)v;  // round to nearest even
+    else p.wp[i] = v;
   }
 }
 }  // namespace
 
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int T, const int* ky,
-                 const int* kx, int Npad, int Kpad, float* wp, hipStream_t s) {
+                 const int* kx, int Npad, int Kpad, float* wp, hipStream_t s, int out_bf16) {
   if (T > IC_MAXT || T < 1) return IC_ERR_ARG;
   PackArgs p;
-  p.W = W; p.wp = wp; p.A = A; p.B = B; p.k = k; p.mode = mode; p.generic = generic; p.T = T;
+  p.W = W; p.wp = wp; p.out_bf16 = out_bf16; p.A = A; p.B = B; p.k = k; p.mode = mode; p.generic = generic; p.T = T;
   p.Npad = Npad; p.Kpad = Kpad;
   for (int t = 0; t < T; ++t) { p.ky[t] = ky[t]; p.kx[t] = kx[t]; }
   const int R = mode == 0 ? B : A;

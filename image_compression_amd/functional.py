@@ -79,7 +79,7 @@ class Conv2dFn(Function):
     """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, act):
+    def forward(ctx, x, weight, bias, stride, padding, act, math=0):
         _lib.require_device(x, weight, bias)
         L = _L()
         x = _cl(x)
@@ -93,18 +93,18 @@ class Conv2dFn(Function):
         Wo = (W + 2 * padding - k) // stride + 1
         y = _new_act(N, Cout, Ho, Wo, x.device)
         ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_conv2d_fwd_ws(ax, k, stride, padding, ay)
+        nb = L.ic_conv2d_fwd_ws_ex(ax, k, stride, padding, ay, int(math))
         buf = _ws(nb, x.device)
-        _lib.check(L.ic_conv2d_fwd(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
-                                   _lib.ptr(buf), nb, _lib.stream_of(x)), "conv2d_fwd")
-        ctx.conf = (stride, padding, k, act, b is not None)
+        _lib.check(L.ic_conv2d_fwd_ex(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act), int(math),
+                                      _lib.ptr(buf), nb, _lib.stream_of(x)), "conv2d_fwd")
+        ctx.conf = (stride, padding, k, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, padding, k, act, has_b = ctx.conf
+        stride, padding, k, act, has_b, math = ctx.conf
         L = _L()
         if act:
             gy = relu_bwd(y, gy)
@@ -116,9 +116,9 @@ class Conv2dFn(Function):
             if x.stride(1) == 1 and dx.stride(1) != 1:
                 dx = dx.contiguous(memory_format=CL)
             ag, adx = _lib.act(gy), _lib.act(dx)
-            nb = L.ic_conv2d_dgrad_ws(ag, k, stride, padding, adx)
+            nb = L.ic_conv2d_dgrad_ws_ex(ag, k, stride, padding, adx, math)
             buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv2d_dgrad(ag, _lib.ptr(w), k, stride, padding, adx, _lib.ptr(buf), nb, st),
+            _lib.check(L.ic_conv2d_dgrad_ex(ag, _lib.ptr(w), k, stride, padding, adx, math, _lib.ptr(buf), nb, st),
                        "conv2d_dgrad")
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
             dw = torch.empty_like(w)
@@ -128,7 +128,7 @@ class Conv2dFn(Function):
             buf = _ws(nb, gy.device)
             _lib.check(L.ic_conv2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
                                          _lib.ptr(buf), nb, st), "conv2d_wgrad")
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 class ConvTranspose2dFn(Function):
@@ -136,7 +136,7 @@ class ConvTranspose2dFn(Function):
     output_padding is implied by `out_hw`."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, output_padding, act):
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, act, math=0):
         _lib.require_device(x, weight, bias)
         L = _L()
         x = _cl(x)
@@ -150,18 +150,19 @@ class ConvTranspose2dFn(Function):
         Wo = (W - 1) * stride - 2 * padding + k + output_padding
         y = _new_act(N, Cout, Ho, Wo, x.device)
         ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_conv_transpose2d_fwd_ws(ax, k, stride, padding, ay)
+        nb = L.ic_conv_transpose2d_fwd_ws_ex(ax, k, stride, padding, ay, int(math))
         buf = _ws(nb, x.device)
-        _lib.check(L.ic_conv_transpose2d_fwd(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
-                                             _lib.ptr(buf), nb, _lib.stream_of(x)), "conv_transpose2d_fwd")
-        ctx.conf = (stride, padding, k, act, b is not None)
+        _lib.check(L.ic_conv_transpose2d_fwd_ex(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
+                                                int(math), _lib.ptr(buf), nb, _lib.stream_of(x)),
+                   "conv_transpose2d_fwd")
+        ctx.conf = (stride, padding, k, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, padding, k, act, has_b = ctx.conf
+        stride, padding, k, act, has_b, math = ctx.conf
         L = _L()
         if act:
             gy = relu_bwd(y, gy)
@@ -171,10 +172,10 @@ class ConvTranspose2dFn(Function):
         if ctx.needs_input_grad[0]:
             dx = _new_act(*x.shape, x.device)
             ag, adx = _lib.act(gy), _lib.act(dx)
-            nb = L.ic_conv_transpose2d_dgrad_ws(ag, k, stride, padding, adx)
+            nb = L.ic_conv_transpose2d_dgrad_ws_ex(ag, k, stride, padding, adx, math)
             buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv_transpose2d_dgrad(ag, _lib.ptr(w), k, stride, padding, adx, _lib.ptr(buf),
-                                                   nb, st), "conv_transpose2d_dgrad")
+            _lib.check(L.ic_conv_transpose2d_dgrad_ex(ag, _lib.ptr(w), k, stride, padding, adx, math,
+                                                      _lib.ptr(buf), nb, st), "conv_transpose2d_dgrad")
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
             dw = torch.empty_like(w)
             db = torch.empty(w.shape[1], device=w.device, dtype=w.dtype) if has_b else None
@@ -183,15 +184,20 @@ class ConvTranspose2dFn(Function):
             buf = _ws(nb, gy.device)
             _lib.check(L.ic_conv_transpose2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
                                                    _lib.ptr(buf), nb, st), "conv_transpose2d_wgrad")
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, act=0):
-    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), int(act))
+MATH = {"fp32": 0, "bf16": 1}   # include/imgcomp.h IC_MATH_*
 
 
-def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, act=0):
-    return ConvTranspose2dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), int(act))
+def conv2d(x, weight, bias=None, stride=1, padding=0, act=0, math=0):
+    """`math`: 0 fp32 (default), 1 bf16 operands with fp32 accumulation (fwd and dgrad)."""
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), int(act), int(math))
+
+
+def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, act=0, math=0):
+    return ConvTranspose2dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), int(act),
+                                   int(math))
 
 
 # ============================================================== GDN

@@ -18,6 +18,8 @@ def _square(v, what):
 
 
 class Conv2d(nn.Conv2d):
+    math = 0   # IC_MATH_*: 0 fp32, 1 bf16 operands / fp32 accumulation (set_compute_dtype)
+
     def __init__(self, *args, **kw):
         super().__init__(*args, **kw)
         if self.groups != 1 or _square(self.dilation, "dilation") != 1 or self.padding_mode != "zeros":
@@ -25,10 +27,13 @@ class Conv2d(nn.Conv2d):
         _square(self.kernel_size, "kernel")
 
     def forward(self, x):
-        return conv2d(x, self.weight, self.bias, _square(self.stride, "stride"), _square(self.padding, "padding"))
+        return conv2d(x, self.weight, self.bias, _square(self.stride, "stride"), _square(self.padding, "padding"),
+                      math=self.math)
 
 
 class ConvTranspose2d(nn.ConvTranspose2d):
+    math = 0
+
     def __init__(self, *args, **kw):
         super().__init__(*args, **kw)
         if self.groups != 1 or _square(self.dilation, "dilation") != 1:
@@ -39,7 +44,8 @@ class ConvTranspose2d(nn.ConvTranspose2d):
         if output_size is not None:
             raise NotImplementedError("output_size is not supported; use output_padding")
         return conv_transpose2d(x, self.weight, self.bias, _square(self.stride, "stride"),
-                                _square(self.padding, "padding"), _square(self.output_padding, "output_padding"))
+                                _square(self.padding, "padding"), _square(self.output_padding, "output_padding"),
+                                math=self.math)
 
 
 class ReLU(nn.ReLU):

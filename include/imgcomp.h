@@ -83,6 +83,27 @@ size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, in
 int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad,
                               float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- math modes of the conv fwd / dgrad "_ex" variants (the plain entry points are math 0).
+ *      IC_MATH_BF16: operands rounded to bf16 (round-to-nearest-even), fp32 accumulation on
+ *      v_mfma_f32_32x32x16_bf16 — the bf16 configuration of BASELINE config C3 — for layers
+ *      whose reduction channel count is a multiple of 64; others (the 3-channel image edges)
+ *      and all weight gradients / GDN stay fp32. */
+#define IC_MATH_FP32 0
+#define IC_MATH_BF16 1
+size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
+int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                     const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
+size_t ic_conv2d_dgrad_ws_ex(const ic_act* dy, int k, int stride, int pad, const ic_act* dx, int math);
+int ic_conv2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int pad, const ic_act* dx,
+                       int math, void* ws, size_t ws_bytes, void* stream);
+size_t ic_conv_transpose2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
+int ic_conv_transpose2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
+                               const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
+size_t ic_conv_transpose2d_dgrad_ws_ex(const ic_act* dy, int k, int stride, int pad, const ic_act* dx,
+                                       int math);
+int ic_conv_transpose2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int pad,
+                                 const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- GDN: norm = beta + conv1x1(x^2, gamma); y = x / sqrt(norm) (inverse: x * sqrt(norm)).
  *      gamma [C][C], beta [C] (already re-parameterised); x, y, norm share one layout. */
 size_t ic_gdn_fwd_ws(const ic_act* x);
