@@ -34,11 +34,33 @@ STEP_GFLOP_PER_IMG = 3 * 2 * FWD_GMAC_PER_IMG   # fwd + dgrad + wgrad = 73.70
 METRIC = "256x256 images/s fwd+bwd at 1/2/4/8 GPUs; bpp & PSNR vs ref on Kodak"
 
 
-def _cfg(lam=256.0):
+# BASELINE.json configs.  C2 is the metric's workload and the
+# default; the others select the same path at their own lambda / loss / width /
+# precision / size (per-GPU batch for weak scaling; C4 = 64 over 4 GPUs, C5 =
+# 128 over 8 GPUs).
+CONFIGS = {
+    "C2": dict(desc="psnr_256 (lambda=256, MSE, Laplacian conditional, 192/192 ch), fp32",
+               lam=256.0, loss=["MSE"], latent=192, dtype="fp32", batch=32, size=256, gflop=73.70),
+    "C3": dict(desc="psnr_4096 (lambda=4096, MSE, latent 320), bf16 operands / fp32 accumulation",
+               lam=4096.0, loss=["MSE"], latent=320, dtype="bf16", batch=32, size=256, gflop=76.27),
+    "C4": dict(desc="ssim_64 (lambda=64, MS-SSIM log-scale loss), fp32",
+               lam=64.0, loss=["MS_SSIMLoss"], latent=192, dtype="fp32", batch=16, size=256, gflop=74.55),
+    "C5": dict(desc="psnr_8192 (lambda=8192, MSE), 512x512 crops, fp32",
+               lam=8192.0, loss=["MSE"], latent=192, dtype="fp32", batch=16, size=512, gflop=73.70),
+}
+
+
+def _cfg(lam=256.0, conf=None):
     from image_compression_amd import get_cfg_defaults
     cfg = get_cfg_defaults()
     cfg.MODEL.LOSS.REDUCTION = "mean"
     cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT = lam
+    if conf is not None:
+        cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT = conf["lam"]
+        cfg.MODEL.LOSS.DISTORTION_LOSS_NAMES = list(conf["loss"])
+        cfg.MODEL.LOSS.SSIM.LOG_SCALE = True      # the ssim_* configs
+        cfg.MODEL.LATENT_CHANNELS = conf["latent"]
+        cfg.MODEL.COMPUTE_DTYPE = conf["dtype"]
     return cfg
 
 
@@ -142,8 +164,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload (C2 = the metric's; default)")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
+    ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-step-only", action="store_true",
@@ -154,6 +178,9 @@ def main():
                          "overlapped with the backward).  Measured equal at N=1: the GPU, not the host, "
                          "paces the launches.")
     args = ap.parse_args()
+    conf = CONFIGS[args.config]
+    args.batch = args.batch or conf["batch"]
+    args.size = args.size or conf["size"]
 
     from image_compression_amd import distributed as D
     from image_compression_amd import modelling
@@ -161,7 +188,7 @@ def main():
     dist = world > 1
     from image_compression_amd.step import TrainStep
     torch.manual_seed(0)
-    model = modelling.build_model(_cfg()).to(dev).train()
+    model = modelling.build_model(_cfg(conf=conf)).to(dev).train()
     # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
@@ -191,8 +218,9 @@ def main():
     torch.cuda.synchronize()
     D.barrier(dev)
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
-    avg = D.mean_over_ranks({"bpp": losses["bpp"], "MSE": losses["MSE"]}, dev)
-    bpp, mse = avg["bpp"], avg["MSE"]
+    dname = conf["loss"][0]
+    avg = D.mean_over_ranks({"bpp": losses["bpp"], dname: losses[dname]}, dev)
+    bpp, dist_val = avg["bpp"], avg[dname]
     if args.profile_step_only:
         if rank == 0:
             print(json.dumps({"ms_per_step": 1e3 * elapsed / args.steps}))
@@ -203,27 +231,29 @@ def main():
     images = args.batch * world * args.steps
     value = images / elapsed
     ms = 1e3 * elapsed / args.steps
-    roof = None if args.no_roofline else dominant_kernel_roofline(dev)
+    roof = None if (args.no_roofline or args.config != "C2") else dominant_kernel_roofline(dev)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline()
     if rank == 0:
-        step_tflops = value / world * STEP_GFLOP_PER_IMG * (args.size / 256) ** 2 / 1e3
+        # model FLOPs per image (3 x forward MACs x 2), x4 per 512^2 image
+        step_tflops = value / world * conf["gflop"] * (args.size / 256) ** 2 / 1e3
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": conf["dtype"],
             "data": "synthetic: torch.rand uniform [0,1) images resident in HBM; random-init weights "
                     "(reference init, seed 0); training noise from in-kernel Philox",
-            "config": {"workload": "C2: psnr_256 (lambda=256, MSE, Laplacian conditional, 192/192 ch), "
+            "config": {"workload": f"{args.config}: {conf['desc']}, "
                                    f"{args.size}x{args.size}, {args.batch} images/GPU, fwd+loss+bwd"
                                    + (" + grad all-reduce" if dist else "") + f" [{mode}]",
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(step_tflops, 2),
             "model_mfma_frac": round(step_tflops / FP32_PEAK_TFLOPS, 4),
-            "bpp": round(bpp, 4), "mse": mse,
+            "bpp": round(bpp, 4), dname.lower(): dist_val,
             "optimizer_step_ms": opt_ms,
+            "images_256_equiv_per_s": round(value * (args.size / 256) ** 2, 2),
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(rec))
