@@ -28,14 +28,23 @@ def env_ranks():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def setup(backend=None):
+def setup(backend=None, device_type=None):
     """Initialise the process group when WORLD_SIZE > 1 and pick this rank's
-    device.  Returns (rank, world, device)."""
+    device.  Returns (rank, world, device).
+
+    backend: None -> "nccl" (RCCL) on GPUs, "gloo" on CPU; IMGCOMP_DIST_BACKEND
+    overrides it (e.g. gloo over GPU tensors to rehearse several ranks on one
+    GPU).  device_type: "cuda" / "cpu" (default: cuda when available).  When
+    there are fewer GPUs than local ranks (rehearsal only), ranks share GPUs
+    round-robin."""
     rank, world, local = env_ranks()
-    use_gpu = backend != "gloo" and torch.cuda.is_available()
+    backend = os.environ.get("IMGCOMP_DIST_BACKEND", backend)
+    use_gpu = (device_type or ("cuda" if torch.cuda.is_available() else "cpu")) == "cuda"
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        ndev = torch.cuda.device_count()
+        dev_idx = local % ndev if ndev else local
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
@@ -92,7 +101,7 @@ def mean_over_ranks(values, device):
 
 def barrier(device):
     if dist.is_initialized() and dist.get_world_size() > 1:
-        if device.type == "cuda":
+        if device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

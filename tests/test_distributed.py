@@ -64,14 +64,17 @@ def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from image_compression_amd import distributed as D
-    r, w, dev = D.setup("gloo")
+    r, w, dev = D.setup("gloo", device_type="cpu")
     assert (r, w, dev.type) == (rank, world, "cpu")
     torch.set_num_threads(2)
     model = D.wrap(OracleModel(_params()), dev, bucket_cap_mb=1.0)
     assert isinstance(model, torch.nn.parallel.DistributedDataParallel)
     x, uz, uy = (D.shard(t, rank, world) for t in _inputs())
-    losses = model(x, uz, uy)
-    losses["total_loss"].backward()
+    # two iterations: DDP raises on the second if any parameter went unused
+    for _ in range(2):
+        model.zero_grad(set_to_none=True)
+        losses = model(x, uz, uy)
+        losses["total_loss"].backward()
     grads = {k: p.grad.detach().clone() for k, p in model.module.named_parameters()}
     mean = D.mean_over_ranks({"total_loss": losses["total_loss"], "bpp": losses["bpp"]}, dev)
     t = D.max_over_ranks(float(rank + 1), dev)
