@@ -11,6 +11,8 @@ import torch  # noqa: F401  (must be imported first: shares its HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libimgcomp.so")
+# kernel-development override (A/B variants of the in-tree library)
+LIB_PATH = os.environ.get("IMGCOMP_LIB") or LIB_PATH
 
 c_int, c_ll, c_ull, c_size, c_float, c_void = (ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                               ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p)

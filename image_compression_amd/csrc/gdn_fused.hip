@@ -235,6 +235,20 @@ __device__ __forceinline__ void bar_wait_lgkm() {
   __builtin_amdgcn_s_barrier();
 }
 
+#ifdef GDN_PROF  // per-phase timestamps (tools/gdn_prof.hip only)
+__device__ unsigned long long gdn_prof[256 * 8 * 16 * 6];
+#define GDN_MARK(it, ev)                                                                         \
+  do {                                                                                           \
+    if (blockIdx.x < 256 && (threadIdx.x & 63) == 0 && (it) < 16)                                \
+      gdn_prof[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 16 + (it)) * 6 + (ev)] =                 \
+          __builtin_amdgcn_s_memtime();                                                          \
+  } while (0)
+#else
+#define GDN_MARK(it, ev) \
+  do {                   \
+  } while (0)
+#endif
+
 // 8 waves, specialised (two per SIMD): waves 0-3 (group A) stage the tiles,
 // form dx by a GEMM with gamma held in VGPRs and copy it out; waves 4-7
 // (group B) accumulate dgamma (C x C, in VGPRs) and dbeta.  The groups run
@@ -281,19 +295,22 @@ __global__ void __launch_bounds__(512, 2)
     };
     uint32_t tile = blockIdx.x;
     if (tile < ntiles) stage(tile, 0);
-    int buf = 0;
+    int buf = 0, it = 0;
     bool first = true;
-    for (; tile < ntiles; tile += gridDim.x) {
+    for (; tile < ntiles; tile += gridDim.x, ++it) {
       if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
       __builtin_amdgcn_s_barrier();  // B1
+      GDN_MARK(it, 0);
       first = false;
       const uint32_t nxt = tile + gridDim.x;
       if (nxt < ntiles) stage(nxt, buf ^ 1);
       float* xs = lds + buf * 3 * TILE;
       float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
       gdn_bwd_phase_a<C, BM>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid);
+      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
+      GDN_MARK(it, 2);
       floatx4v acc[NTW];
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
@@ -306,6 +323,7 @@ __global__ void __launch_bounds__(512, 2)
           for (int j = 0; j < NTW; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[v], bfr[j][4 * u + v], acc[j], 0, 0, 0);
       }
+      GDN_MARK(it, 3);
       // dx = direct + 2 x dxg over the direct term (each element owned by one lane); m = 4lq + r
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
@@ -316,7 +334,9 @@ __global__ void __launch_bounds__(512, 2)
           gs[off] = gs[off] + 2.f * xs[off] * acc[j][r];
         }
       }
+      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
+      GDN_MARK(it, 5);
       store_tile<C, BM, NTA>(dx, tile * BM, P, gs, tid);
       buf ^= 1;
     }
@@ -330,20 +350,27 @@ __global__ void __launch_bounds__(512, 2)
     float db = 0.f;  // dbeta[t] partial, t = tid - 256 < C
     const int t = tid - 256;
     int buf = 0;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int it = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
+      GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
       gdn_bwd_phase_a<C, BM>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid);
+      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
+      GDN_MARK(it, 2);
       if (t < C) {
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
       }
 #pragma unroll
       for (int s2 = 0; s2 < BM / 4; ++s2) {
-        const int m = 4 * s2 + lq;  // k-step s2 of the pixel reduction
+        // k-step s2 of the pixel reduction takes pixel m = 4 lq + s2 (any order
+        // works, A and B agree): the 4 lane quads then read rows differing in
+        // bits 2-3, which the row swizzle sends to distinct banks
+        const int m = 4 * lq + s2;
         float a[NTW];
 #pragma unroll
         for (int i = 0; i < NTW; ++i) a[i] = qs[swz<C>(m, wbase + 16 * i + li)];
@@ -356,7 +383,10 @@ __global__ void __launch_bounds__(512, 2)
             dg[i][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b, dg[i][kt], 0, 0, 0);
         }
       }
+      GDN_MARK(it, 3);
+      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
+      GDN_MARK(it, 5);
       buf ^= 1;
     }
     // partials: slab[block][n][k] (C*C) then dbeta [C]

@@ -182,8 +182,9 @@ __global__ void __launch_bounds__(256, 2) ig_kernel(const IgDesc d) {
   do {                                                                                            \
     const int c__ = (c_);                                                                         \
     if constexpr (!GEN) {                                                                         \
-      const int cpt = d.Cin >> 5;                                                                 \
-      const int t = c__ / cpt, cc = c__ - t * cpt;                                                \
+      /* channel chunk outer, tap inner: a pixel's chunk is re-read by the next */               \
+      /* taps while it is still in L2 (tap-outer re-reads it ~T times from HBM) */                \
+      const int cc = c__ / P.T, t = c__ - cc * P.T;                                               \
       const int dy = P.dy[t], dx = P.dx[t];                                                       \
       const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);         \
       _Pragma("unroll") for (int p = 0; p < APASS; ++p) {                                         \
@@ -341,7 +342,7 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
   floatx4v ra[APASS];
   bf16x8 rb[BPASS];
   auto gload = [&](int c) {
-    const int t = c / cpt, cc = c - t * cpt;
+    const int cc = c / P.T, t = c - cc * P.T;  // channel chunk outer, tap inner (L2 reuse)
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 64 + ac4 * 4);
 #pragma unroll

@@ -20,7 +20,12 @@ PEAK = 157.3
 CL = torch.channels_last
 
 
-def t_ms(fn, reps):
+ONLY = None
+
+
+def t_ms(fn, reps, tag=None):
+    if ONLY is not None and tag is not None and ONLY not in tag:
+        return float("nan")
     fn()
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
@@ -45,7 +50,10 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="run only ops whose 'layer op' contains this text")
     a = ap.parse_args()
+    global ONLY
+    ONLY = a.only
     L = _lib.load()
     st = _lib.c_void(torch.cuda.current_stream().cuda_stream)
     N, S = a.batch, a.size
@@ -77,18 +85,18 @@ def main():
         wg, wgws = getattr(L, pref + "_wgrad"), getattr(L, pref + "_wgrad_ws")
         n1 = fws(ax, k, s, p, ay)
         b1 = ws(n1)
-        ms = t_ms(lambda: _lib.check(fwd(ax, _lib.ptr(w), _lib.ptr(b), k, s, p, ay, 0, _lib.ptr(b1), n1, st), "fwd"), a.reps)
+        ms = t_ms(lambda: _lib.check(fwd(ax, _lib.ptr(w), _lib.ptr(b), k, s, p, ay, 0, _lib.ptr(b1), n1, st), "fwd"), a.reps, name + " fwd")
         rows.append((name, "fwd", ms, gf))
         if not (name.startswith("g_a.0")):
             n2 = dgws(ay, k, s, p, ax)
             b2 = ws(n2)
-            ms = t_ms(lambda: _lib.check(dg(ay, _lib.ptr(w), k, s, p, ax, _lib.ptr(b2), n2, st), "dgrad"), a.reps)
+            ms = t_ms(lambda: _lib.check(dg(ay, _lib.ptr(w), k, s, p, ax, _lib.ptr(b2), n2, st), "dgrad"), a.reps, name + " dgrad")
             rows.append((name, "dgrad", ms, gf))
         dw = torch.empty_like(w)
         db = torch.empty(cout, device="cuda")
         n3 = wgws(ax, ay, k, s, p)
         b3 = ws(n3)
-        ms = t_ms(lambda: _lib.check(wg(ax, ay, k, s, p, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(b3), n3, st), "wgrad"), a.reps)
+        ms = t_ms(lambda: _lib.check(wg(ax, ay, k, s, p, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(b3), n3, st), "wgrad"), a.reps, name + " wgrad")
         rows.append((name, "wgrad", ms, gf))
 
     def gdn_layer(name, c, h):
@@ -102,7 +110,7 @@ def main():
         gf = 2.0 * N * h * h * c * c / 1e9
         n1 = L.ic_gdn_fwd_ws(ax)
         b1 = ws(n1)
-        ms = t_ms(lambda: _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(be), 0, ay, _lib.ptr(nrm), _lib.ptr(b1), n1, st), "gdn"), a.reps)
+        ms = t_ms(lambda: _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(be), 0, ay, _lib.ptr(nrm), _lib.ptr(b1), n1, st), "gdn"), a.reps, name + " gdn_fwd")
         rows.append((name, "gdn_fwd", ms, gf))
         dx = torch.empty_like(x)
         dg = torch.empty_like(g)
@@ -110,7 +118,7 @@ def main():
         n2 = L.ic_gdn_bwd_ws(ax)
         b2 = ws(n2)
         ms = t_ms(lambda: _lib.check(L.ic_gdn_bwd(ax, _lib.ptr(nrm), _lib.ptr(gy), _lib.ptr(g), 0, _lib.act(dx), _lib.ptr(dg),
-                                                  _lib.ptr(dbe), _lib.ptr(b2), n2, st), "gdnb"), a.reps)
+                                                  _lib.ptr(dbe), _lib.ptr(b2), n2, st), "gdnb"), a.reps, name + " gdn_bwd")
         rows.append((name, "gdn_bwd", ms, 2 * gf))
 
     h = S
@@ -138,6 +146,9 @@ def main():
     tot_ms = sum(r[2] for r in rows)
     tot_gf = sum(r[3] for r in rows)
     print(f"{'layer':22s} {'op':8s} {'ms':>8s} {'GFLOP':>8s} {'TF/s':>7s} {'frac':>6s}")
+    rows = [r for r in rows if r[2] == r[2]]  # drop skipped (nan) ops
+    tot_ms = sum(r[2] for r in rows)
+    tot_gf = sum(r[3] for r in rows)
     for name, op, ms, gf in rows:
         tf = gf / ms
         print(f"{name:22s} {op:8s} {ms:8.3f} {gf:8.1f} {tf:7.1f} {tf / PEAK:6.3f}")
