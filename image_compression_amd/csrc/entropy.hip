@@ -163,7 +163,7 @@ __global__ void fact_fwd_k(const float* z, long long n, int C, const ic_fact_par
   }
 }
 
-__global__ void fact_bwd_k(const float* qin, long long n, int C, const ic_fact_params P,
+__global__ void __launch_bounds__(256) fact_bwd_k(const float* qin, long long n, int C, const ic_fact_params P,
                            const float* dq, const float* dp, float* dz, const ic_fact_grads GR, int round_mode) {
   __shared__ float lds[16 * NG];
   const int c = blockIdx.x;

@@ -413,8 +413,18 @@ __global__ void ig_reduce_kernel(const IgDesc d) {
        i += (long long)gridDim.x * blockDim.x) {
     const long long mg = i / d.Cout;
     const int n = (int)(i - mg * d.Cout);
-    float v = 0.f;
-    for (int s = 0; s < d.ksplit; ++s) v += d.partial[((long long)s * d.Mtot + mg) * d.Cout + n];
+    // eight independent loads in flight (a serial chain waits one memory
+    // latency per split); fixed order, so the sum is deterministic
+    const float* src = d.partial + i;
+    const long long ss = d.Mtot * d.Cout;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 7 < d.ksplit; s += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += src[(s + j) * ss];
+    }
+    for (int j = 0; s < d.ksplit; ++s, ++j) a[j] += src[s * ss];
+    const float v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     int ph = 0;
 #pragma unroll
     for (int q = 1; q < IC_MAXPH; ++q)
@@ -453,6 +463,10 @@ int ig_npad(int Cout) {
   return (Cout + 31) / 32 * 32;
 }
 
+#ifndef IG_KSPLIT_MAX
+#define IG_KSPLIT_MAX 32  // more splits cost more in the partial-sum pass than they save
+#endif
+
 size_t ig_plan(IgDesc& d) {
   if (d.Cout % 192 == 0) { d.bm = 128; d.bn = 192; }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
@@ -478,7 +492,8 @@ size_t ig_plan(IgDesc& d) {
   int ksplit = 1;
   if (tiles < 512 && nchunks_max >= 4) {
     ksplit = (int)((1024 + tiles - 1) / tiles);
-    const int maxs = nchunks_max / 2;
+    int maxs = nchunks_max / 2;
+    if (maxs > IG_KSPLIT_MAX) maxs = IG_KSPLIT_MAX;
     if (ksplit > maxs) ksplit = maxs;
     if (ksplit < 1) ksplit = 1;
   }
