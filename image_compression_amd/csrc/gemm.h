@@ -80,6 +80,7 @@ struct WgDesc {
   long long P;     // N*Hg*Wg
   int pps, nsplit; // pixels per split, number of splits
   FastDiv fd_hw, fd_w;  // divide a pixel index by Hg*Wg and by Wg (set by wg_run)
+  int rowfast;     // Wg and pixels-per-split multiples of the 16-pixel K step (set by wg_run)
   float* partial;  // [nsplit][Tp][Cg][ncols]
   int dy[IC_MAXT], dx[IC_MAXT];
 };

@@ -235,9 +235,59 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dyt = d.dy[t], dxt = d.dx[t];
 
+  // Row-fast staging (d.rowfast): a 16-pixel K step never crosses an output
+  // row, so image / output row / first column are uniform per step (scalar
+  // unit) and each lane only adds its constant row and column offsets: a few
+  // VALU per LDS-DMA instead of two divisions and three 64-bit products.
+  int goff[GPASS], xoff[XPASS], xix[XPASS];
+  bool gok[GPASS], xok[XPASS];
+#pragma unroll
+  for (int q = 0; q < GPASS; ++q) {
+    const int f = tid + 256 * q;
+    const int row = f / G4, c4 = (f - (f / G4) * G4) ^ ((row & 1) << 3);
+    const int col = g0 + c4 * 4;
+    gok[q] = col < d.Cg;
+    goff[q] = row * (int)d.gs_w + col;
+  }
+#pragma unroll
+  for (int q = 0; q < XPASS; ++q) {
+    const int f = tid + 256 * q;
+    const int row = f / X4, c4 = (f - (f / X4) * X4) ^ ((row & 1) << 3);
+    const int col = c0 + c4 * 4;
+    xok[q] = col < d.Cx;
+    xix[q] = row * d.stride;
+    xoff[q] = row * d.stride * (int)d.xs_w + col;
+  }
+
   auto stage = [&](uint32_t p0, int buf) {
     float* Gs = lds + buf * STAGE;
     float* Xs = Gs + BK * BM;
+    if (d.rowfast) {
+      const uint32_t img = fdiv(p0, d.fd_hw);
+      const uint32_t rr = p0 - img * d.fd_hw.d;
+      const uint32_t gy = fdiv(rr, d.fd_w);
+      const uint32_t gx0 = rr - gy * d.fd_w.d;
+      const float* gb = d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w;
+      const int iy = (int)gy * d.stride + dyt, ix0 = (int)gx0 * d.stride + dxt;
+      const bool rowok = (unsigned)iy < (unsigned)d.Hx;
+      const float* xb = d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h + (long long)ix0 * d.xs_w;
+#pragma unroll
+      for (int q = 0; q < GPASS; ++q) {
+        const int f = tid + 256 * q;
+        const float* src = gok[q] ? gb + goff[q] : wg_zero_page;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Gs + (f - lane) * 4), 16, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < XPASS; ++q) {
+        const int f = tid + 256 * q;
+        const bool ok = rowok && xok[q] && (unsigned)(ix0 + xix[q]) < (unsigned)d.Wx;
+        const float* src = ok ? xb + xoff[q] : wg_zero_page;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Xs + (f - lane) * 4), 16, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < GPASS; ++q) {
       const int f = tid + 256 * q;
@@ -532,6 +582,8 @@ int wg_run(WgDesc& d, hipStream_t s) {
   if (d.P == 0) return IC_OK;
   if (d.P >= (1LL << 31)) return IC_ERR_ARG;  // 32-bit pixel indexing
   d.fd_hw = make_fastdiv((uint32_t)((long long)d.Hg * d.Wg));
+  d.rowfast = d.Wg % 16 == 0 && d.pps % 16 == 0 && d.gs_w * 16 < (1LL << 31) &&
+              (long long)d.stride * 16 * d.xs_w < (1LL << 31);
   d.fd_w = make_fastdiv((uint32_t)d.Wg);
   d.g_vec = (d.gs_c == 1 && d.Cg % 4 == 0);
   // LDS-DMA path: 16-B aligned float4 rows in both operands
