@@ -468,7 +468,14 @@ int ig_npad(int Cout) {
 #endif
 
 size_t ig_plan(IgDesc& d) {
-  if (d.Cout % 192 == 0) { d.bm = 128; d.bn = 192; }
+  long long mall = 0;
+  for (int p = 0; p < d.nphase; ++p) mall += (long long)d.N * d.ph[p].Hg * d.ph[p].Wg;
+  if (d.Cout % 192 == 0) {
+    // small maps (hyperprior, 16x16 and below): 64-row tiles double the tile
+    // grid, so fewer K splits (and less split-K partial traffic) fill the chip
+    d.bm = (!d.bf16 && mall < 32768) ? 64 : 128;
+    d.bn = 192;
+  }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
   else { d.bm = 256; d.bn = 32; }
   d.Npad = ig_npad(d.Cout);
@@ -513,7 +520,8 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.bf16 && (d.generic || d.Cin % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
-  if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
+  if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
+  else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);
   else rc = ig_launch_t<256, 32, 64, 32>(d, s);
   if (rc) return rc;
