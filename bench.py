@@ -96,7 +96,8 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0):
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4),
             "timing": (f"live: HIP events on the launch stream around the layer's {live_launches} launches "
                        "inside the timed steps" if live_ms else "isolated loop of the same launch"),
-            "isolated_ms_per_launch": round(iso_ms, 4)}
+            "isolated_ms_per_launch": round(iso_ms, 4),
+            "peak_measured": _mfma_peak_measured()}
 
 
 class LiveLaunchTimer:
@@ -170,6 +171,19 @@ def _pmc_traffic():
         return None
     with open(files[-1]) as fh:
         return round(json.load(fh)["traffic_bytes_per_launch"])
+
+
+def _mfma_peak_measured():
+    """Sustained fp32 MFMA rate measured on the box by tools/mfma_peak.hip
+    (committed as profiles/*_mfma_peak.json; SURVEY.md 8d: report the spec
+    peak and the measured one)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_mfma_peak.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        rows = [json.loads(line) for line in fh if line.strip()]
+    return max(r["tflops"] for r in rows) if rows else None
 
 
 def cpu_baseline(seconds_target=12.0):
