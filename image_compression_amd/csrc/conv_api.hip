@@ -38,7 +38,7 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
                   const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
   const int T = k * k;
   const int Kp = (int)ic_align((size_t)T * x->c, 32);
-  if ((epi == EPI_NONE || epi == EPI_RELU) && edge_conv_ok(x->c, k, stride, x->sw, y->sc, y->c)) {
+  if ((epi == EPI_NONE || epi == EPI_RELU) && edge_conv_ok(x->c, k, stride, x->sw, y->sc, y->c, y->sw, y->sh, y->sn)) {
     // patch-gather kernel (edge.hip): no im2col columns in HBM
     const int Npad = ig_npad(y->c);
     const size_t wpb = (size_t)Npad * Kp * 4;

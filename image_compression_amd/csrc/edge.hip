@@ -124,9 +124,14 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) bfr[j][s] = (s < KS && kk < Kp) ? wp[(size_t)(nbase + 16 * j + li) * Kp + kk] : 0.f;
   }
-  float bv[NTW];
+  // D = W * patch^T (weights as the A operand): lane (li, lq) then holds four
+  // consecutive output channels n = nbase + 16j + 4lq + r of pixel li, so each
+  // (pixel, channel quad) leaves as one 16-B store
+  floatx4v bv[NTW];
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) bv[j] = bias ? bias[nbase + 16 * j + li] : 0.f;
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
   // zero runs after both patch buffers
   for (int i = tid; i < 2 * SEG * 2; i += 256) {
     lds[PSZ + i] = 0.f;
@@ -158,31 +163,32 @@ __global__ void __launch_bounds__(256, 2)
           const float a = patch[koff[s] + g.stride * (16 * mt + li)];
 #pragma unroll
           for (int j = 0; j < NTW; ++j)
-            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bfr[j][s], acc[mt][j], 0, 0, 0);
+            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][s], a, acc[mt][j], 0, 0, 0);
         }
       }
     }
-    // epilogue: C/D map col n = li, row m = 4lq + r
+    // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li)
     const int seg = (int)(u % g.units_per_row);
     const long long rr = u / g.units_per_row;
     const int oy = (int)(rr % g.Ho);
     const int n = (int)(rr / g.Ho);
     const int ox0 = seg * SEG;
-    float* yb = y + n * ys_n + (long long)oy * ys_h;
+    float* yb = y + n * ys_n + (long long)oy * ys_h + nbase + 4 * lq;
 #pragma unroll
-    for (int mt = 0; mt < SEG / 16; ++mt)
+    for (int mt = 0; mt < SEG / 16; ++mt) {
+      const int ox = ox0 + 16 * mt + li;
+      if (ox < g.Wo) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ox = ox0 + 16 * mt + 4 * lq + r;
-        if (ox < g.Wo) {
+        for (int j = 0; j < NTW; ++j) {
+          floatx4v v = acc[mt][j] + bv[j];
+          if (relu) {
 #pragma unroll
-          for (int j = 0; j < NTW; ++j) {
-            float v = acc[mt][j][r] + bv[j];
-            if (relu) v = v > 0.f ? v : 0.f;
-            yb[(long long)ox * ys_w + nbase + 16 * j + li] = v;
+            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
           }
+          *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = v;
         }
       }
+    }
     if (un < g.units) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
     buf ^= 1;
   }
@@ -346,7 +352,8 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
                   long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s) {
   EdgeGeom g;
   if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
-  if (ys_c != 1 || Kp < g.TC) return IC_ERR_ARG;
+  // 16-B channel-quad stores
+  if (ys_c != 1 || Kp < g.TC || ((uintptr_t)y & 15) || ys_w % 4 || ys_h % 4 || ys_n % 4) return IC_ERR_ARG;
   const int grid = edge_grid(g.units, 2);
   if (grid < 1) return IC_OK;
   switch (Cout) {
@@ -369,9 +376,10 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
   return IC_OK;
 }
 
-bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout) {
+bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,
+                  long long ys_n) {
   return C >= 1 && C <= 4 && k <= 5 && k * k * C <= KMAX && stride >= 1 && stride <= 2 && sw == 1 && ys_c == 1 &&
-         (Cout == 64 || Cout == 128 || Cout == 192);
+         (Cout == 64 || Cout == 128 || Cout == 192) && ys_w % 4 == 0 && ys_h % 4 == 0 && ys_n % 4 == 0;
 }
 
 // workspace of edge_wgrad_run

@@ -121,7 +121,8 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s);
 
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
-bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout);
+bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,
+                  long long ys_n);
 int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H, int W,
                   const float* wp, int Kp, const float* bias, int k, int stride, int pad, float* y, long long ys_n,
                   long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s);
