@@ -230,6 +230,16 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
   }
 }
 
+// Keep a k-step's MFMAs inside that step: IR-level code motion otherwise sinks
+// chains of them to the end of an unrolled loop, which keeps every step's
+// operand fragments live (sched_barrier only constrains the machine
+// scheduler).  Emits no instructions.
+template <int N>
+__device__ __forceinline__ void pin_acc(floatx4v* a) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+}
+
 __device__ __forceinline__ void bar_wait_lgkm() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -304,7 +314,6 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 0);
       first = false;
       const uint32_t nxt = tile + gridDim.x;
-      if (nxt < ntiles) stage(nxt, buf ^ 1);
       float* xs = lds + buf * 3 * TILE;
       float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
       gdn_bwd_phase_a<C, BM>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid);
@@ -322,6 +331,13 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
           for (int j = 0; j < NTW; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[v], bfr[j][4 * u + v], acc[j], 0, 0, 0);
+        if (u == 0) {
+          // the next tile's DMA issues behind the first MFMAs instead of on the
+          // barrier-to-barrier critical path (buffer buf^1 is free since B1)
+          __builtin_amdgcn_sched_barrier(0);
+          if (nxt < ntiles) stage(nxt, buf ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       GDN_MARK(it, 3);
       // dx = direct + 2 x dxg over the direct term (each element owned by one lane); m = 4lq + r
@@ -365,23 +381,40 @@ __global__ void __launch_bounds__(512, 2)
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
       }
+      // k-step s2 of the pixel reduction takes pixel m = 4 lq + s2 (any order
+      // works, A and B agree): the 4 lane quads then read rows differing in
+      // bits 2-3, which the row swizzle sends to distinct banks.  Fragments
+      // are read one k-step ahead of their MFMAs.
+      float a[NTW], b[KT];
+#pragma unroll
+      for (int i = 0; i < NTW; ++i) a[i] = qs[swz<C>(4 * lq, wbase + 16 * i + li)];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) b[kt] = xs[swz<C>(4 * lq, 16 * kt + li)];
 #pragma unroll
       for (int s2 = 0; s2 < BM / 4; ++s2) {
-        // k-step s2 of the pixel reduction takes pixel m = 4 lq + s2 (any order
-        // works, A and B agree): the 4 lane quads then read rows differing in
-        // bits 2-3, which the row swizzle sends to distinct banks
-        const int m = 4 * lq + s2;
-        float a[NTW];
+        float an[NTW], bn[KT];
+        if (s2 + 1 < BM / 4) {
+          const int mn = 4 * lq + s2 + 1;
 #pragma unroll
-        for (int i = 0; i < NTW; ++i) a[i] = qs[swz<C>(m, wbase + 16 * i + li)];
+          for (int i = 0; i < NTW; ++i) an[i] = qs[swz<C>(mn, wbase + 16 * i + li)];
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) bn[kt] = xs[swz<C>(mn, 16 * kt + li)];
+        }
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
-          float b = xs[swz<C>(m, 16 * kt + li)];
-          b = b * b;
+          const float b2 = b[kt] * b[kt];
 #pragma unroll
           for (int i = 0; i < NTW; ++i)
-            dg[i][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b, dg[i][kt], 0, 0, 0);
+            dg[i][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b2, dg[i][kt], 0, 0, 0);
         }
+        if (s2 + 1 < BM / 4) {
+#pragma unroll
+          for (int i = 0; i < NTW; ++i) a[i] = an[i];
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) b[kt] = bn[kt];
+        }
+        pin_acc<NTW * KT>(&dg[0][0]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       GDN_MARK(it, 3);
       GDN_MARK(it, 4);
