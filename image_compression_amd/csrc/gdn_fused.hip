@@ -133,7 +133,6 @@ __global__ void __launch_bounds__(256, 2)
     __builtin_amdgcn_s_barrier();
     first = false;
     const uint32_t nxt = tile + gridDim.x;
-    if (nxt < ntiles) stage_tile<C, BM, NT>(x, nxt * BM, P, lds + (buf ^ 1) * TILE, tid, lane);
     float* xs = lds + buf * TILE;
 
     floatx4v acc[MT][NTW];
@@ -168,6 +167,12 @@ __global__ void __launch_bounds__(256, 2)
         for (int mt = 0; mt < MT; ++mt) a4[mt] = an[mt];
       }
       __builtin_amdgcn_sched_barrier(0);
+      // the next tile's DMA issues behind the first MFMAs, off the
+      // barrier-to-barrier path (buffer buf^1 is free since the barrier)
+      if (u == 0 && nxt < ntiles) {
+        stage_tile<C, BM, NT>(x, nxt * BM, P, lds + (buf ^ 1) * TILE, tid, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     // every wave's x^2 reads are done before y overwrites x in place
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
