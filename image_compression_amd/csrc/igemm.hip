@@ -471,9 +471,9 @@ size_t ig_plan(IgDesc& d) {
   long long mall = 0;
   for (int p = 0; p < d.nphase; ++p) mall += (long long)d.N * d.ph[p].Hg * d.ph[p].Wg;
   if (d.Cout % 192 == 0) {
-    // small maps (hyperprior, 16x16 and below): 64-row tiles double the tile
+    // small maps (hyperprior and <= 32x32 at batch 32): 64-row tiles double the tile
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
-    d.bm = (!d.bf16 && mall < 32768) ? 64 : 128;
+    d.bm = (!d.bf16 && mall < 65536) ? 64 : 128;
     d.bn = 192;
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
