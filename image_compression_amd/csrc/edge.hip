@@ -196,23 +196,25 @@ __global__ void __launch_bounds__(256, 2)
 
 // ------------------------------------------------------------------ wgrad
 // G NHWC-dense [N][Ho][Wo][CG] (pixel stride CG), 16-B aligned; CG in {64,128,192}
-template <int CG>
-__global__ void __launch_bounds__(256, 1)
+// KTMAX = 16-wide k-tiles compiled for (5 covers the 3-channel 5x5 edges plus
+// the ones column: 76 columns)
+template <int CG, int KTMAX>
+__global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     edge_wgrad_kernel(const EdgeGeom g, const float* __restrict__ G, int Kc, int ones, float* __restrict__ slab) {
   constexpr int NTW = CG / 64;            // 16-wide g-tiles per wave
-  constexpr int KTMAX = (KMAX + 1 + 15) / 16;
   constexpr int CH = CG / 4;              // 16-B chunks per G row
   constexpr int GT = SEG * CG;            // G tile floats
   constexpr int QP = SEG * CH / 256;      // LDS-DMA pieces per thread
   constexpr int PB = PMAX + 2 * SEG * 2 + 2 * SEG * 2;  // patch + zero run + ones run
-  __shared__ __attribute__((aligned(16))) float lds[2 * GT + 2 * PB];
+  // one G buffer (two blocks per CU cover each other's staging) and two patch buffers
+  __shared__ __attribute__((aligned(16))) float lds[GT + 2 * PB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int gbase = w * (CG / 4);
   const int KT = (Kc + 15) / 16;
   const int PSZ = g.C * g.k * g.PW;
   const int zero_off = PSZ, ones_off = PSZ + 2 * SEG * 2;
-  float* const pbase = lds + 2 * GT;
+  float* const pbase = lds + GT;
 
   int koff[KTMAX];
 #pragma unroll
@@ -255,13 +257,10 @@ __global__ void __launch_bounds__(256, 1)
     edge_patch_store(g, pr, pbase, tid);
   }
   for (; u < g.units; u += gridDim.x) {
-    __syncthreads();  // vmcnt(0) + barrier: tile `buf` and its patch are in LDS
+    __syncthreads();  // vmcnt(0) + barrier: the G tile and patch `buf` are in LDS
     const long long un = u + gridDim.x;
-    if (un < g.units) {
-      stage_g(un, lds + (buf ^ 1) * GT);
-      edge_patch_load(g, un, pr, tid);
-    }
-    const float* gs = lds + buf * GT;
+    if (un < g.units) edge_patch_load(g, un, pr, tid);
+    const float* gs = lds;
     const float* patch = pbase + buf * PB;
     // k-step s2 of the pixel reduction: pixel m = 4 s2 + lq
 #pragma unroll 4
@@ -282,7 +281,11 @@ __global__ void __launch_bounds__(256, 1)
         }
       }
     }
-    if (un < g.units) edge_patch_store(g, pr, pbase + (buf ^ 1) * PB, tid);
+    __syncthreads();  // every wave is done with the G tile
+    if (un < g.units) {
+      stage_g(un, lds);
+      edge_patch_store(g, pr, pbase + (buf ^ 1) * PB, tid);
+    }
     buf ^= 1;
   }
   // partial [CG][Kc] of this block (C/D map: row = g index 4lq + r, col = k index li)
@@ -384,7 +387,7 @@ bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Co
 
 // workspace of edge_wgrad_run
 size_t edge_wgrad_ws(int CG, int Kc, long long units) {
-  return (size_t)edge_grid(units, 1) * CG * Kc * sizeof(float);
+  return (size_t)edge_grid(units, 2) * CG * Kc * sizeof(float);
 }
 
 bool edge_wgrad_ok(int C, int k, int stride, long long sw, const float* G, int CG, long long gs_c, long long gs_w,
@@ -404,22 +407,26 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
   EdgeGeom g;
   if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
   const int Kc = g.TC + (db ? 1 : 0);
-  const int grid = edge_grid(g.units, 1);
+  const bool k5 = Kc <= 80;  // 5 k-tiles: two blocks per CU
+  const int grid = edge_grid(g.units, k5 ? 2 : 1);
   if (grid < 1) return IC_OK;
   float* slab = (float*)ws;
+#define EDGE_WG(CG_, KT_) \
+  hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_>), dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab)
   switch (CG) {
     case 192:
-      hipLaunchKernelGGL(edge_wgrad_kernel<192>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      if (k5) EDGE_WG(192, 5); else EDGE_WG(192, 7);
       break;
     case 128:
-      hipLaunchKernelGGL(edge_wgrad_kernel<128>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      if (k5) EDGE_WG(128, 5); else EDGE_WG(128, 7);
       break;
     case 64:
-      hipLaunchKernelGGL(edge_wgrad_kernel<64>, dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab);
+      if (k5) EDGE_WG(64, 5); else EDGE_WG(64, 7);
       break;
     default:
       return IC_ERR_ARG;
   }
+#undef EDGE_WG
   IC_CHECK_LAUNCH();
   const int total = CG * Kc;
   hipLaunchKernelGGL(edge_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, grid, CG, Kc, C,
