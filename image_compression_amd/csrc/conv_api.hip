@@ -183,6 +183,13 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if (x->n != y->n) return IC_ERR_ARG;
   if ((y->h + 2 * pad - k) / stride + 1 != x->h || (y->w + 2 * pad - k) / stride + 1 != x->w)
     return IC_ERR_ARG;
+  if ((epi == EPI_NONE || epi == EPI_RELU) &&
+      tconv_few_ok(x->c, y->c, k, stride, pad, x->sc, x->sw, x->sh, x->sn, x->h, x->w)) {
+    // output-row-stationary kernel (edge.hip): no column buffer in HBM
+    if (need) { *need = 0; return IC_OK; }
+    return tconv_few_run(x->data, x->n, x->h, x->w, x->c, W, y->c, k, pad, bias, epi == EPI_RELU, y->data, y->sn,
+                         y->sc, y->sh, y->sw, y->h, y->w, s);
+  }
   if (y->c <= FEW_CH && x->c % 32 == 0 && x->sc == 1)
     return transposed_col2im(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need);
   IgDesc d = {};

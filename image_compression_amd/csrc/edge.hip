@@ -347,6 +347,117 @@ int edge_grid(long long units, int per_cu) {
   return (int)(units < cap ? units : cap);
 }
 
+
+// ------------------------------------------------------------------ tconv to few channels
+// Transposed conv, stride 2, wide NHWC input -> few-channel output (g_s.6:
+// 192 -> 3, 5x5): output-row stationary, no column buffer in HBM.
+//   out[n][o][Y][X] = b[o] + sum_{ky,kx,c} x[n][iy][ix][c] W[c][o][ky][kx],
+//   Y = 2 iy - pad + ky,  X = 2 ix - pad + kx.
+// Output row Y takes the taps ky = (Y + pad) mod 2, +2, ..., each from one
+// input row iy; per (ky, iy) one small GEMM Cm[ix][(kx, o)] = x[n][iy][ix][:] .
+// W[:, o, ky, kx] (M = input width, N = k*Cout <= 16 on one 16-wide MFMA tile,
+// K = Cin) leaves its rows in LDS, and a fixed-order gather sums
+// out[X][o] = sum_{ky, kx: X + pad - kx even} Cm_ky[(X + pad - kx)/2][(kx, o)].
+// Every (ky, iy, ix) product is formed once (no padded MACs beyond N 15 -> 16).
+// Blocks are persistent over rows of one parity of Y (their ky set), with that
+// parity's weights staged once in LDS as B fragments [kyi][u][lq][col][v]:
+// MFMA step s = 4u + v consumes channel 16u + 4lq + v on both sides, so a
+// lane's A operand is one float4 of its pixel's channels.
+constexpr int TF_KY = 3;  // taps per parity for k <= 5
+
+template <int NWV, int MTW>  // waves, 16-pixel m-tiles per wave: input width <= 16 * NWV * MTW
+__global__ void __launch_bounds__(64 * NWV, 2)
+    tconv_few_kernel(const float* __restrict__ x, int N, int Hin, int Win, int Cin, const float* __restrict__ W,
+                     int Cout, int k, int pad, const float* __restrict__ bias, int relu, float* __restrict__ y,
+                     long long ysn, long long ysc, long long ysh, long long ysw, int Hout, int Wout) {
+  constexpr int WMAX = 16 * NWV * MTW;
+  constexpr int NT = 64 * NWV;
+  __shared__ __attribute__((aligned(16))) float wl[TF_KY * 12 * 4 * 16 * 4];  // Cin <= 192
+  __shared__ __attribute__((aligned(16))) float cm[TF_KY * WMAX * 16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int U = Cin >> 4;
+  const int par = blockIdx.x & 1;               // rows Y with Y % 2 == par
+  const int ky0 = (par + pad) & 1;              // their first tap row
+  const int nky = (k - ky0 + 1) >> 1;
+  const int ncol = k * Cout;
+  // weights of this parity: wl[((kyi*U + u)*4 + q)*16 + col][v] = W[c = 16u+4q+v][o][ky][kx], col = kx*Cout + o
+  for (int i = tid; i < nky * U * 4 * 16 * 4; i += NT) {
+    const int v = i & 3, col = (i >> 2) & 15, q = (i >> 6) & 3, r = i >> 8;
+    const int u = r % U, kyi = r / U;
+    const int c = 16 * u + 4 * q + v, ky = ky0 + 2 * kyi;
+    float val = 0.f;
+    if (col < ncol) {
+      const int kx = col / Cout, o = col - (col / Cout) * Cout;
+      val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
+    }
+    wl[i] = val;
+  }
+  const int rows_par = (Hout - par + 1) >> 1;   // rows of this parity per image
+  const long long nrows = (long long)N * rows_par;
+  for (long long rr = blockIdx.x >> 1; rr < nrows; rr += gridDim.x >> 1) {
+    const int n = (int)(rr / rows_par);
+    const int Y = 2 * (int)(rr - (long long)n * rows_par) + par;
+    __syncthreads();  // weights staged / previous row's gather done with cm
+    for (int kyi = 0; kyi < nky; ++kyi) {
+      const int ky = ky0 + 2 * kyi;
+      const int iy = (Y + pad - ky) >> 1;     // Y + pad - ky is even
+      if (iy < 0 || iy >= Hin) continue;      // uniform: no contribution
+      const float* xr = x + ((size_t)n * Hin + iy) * Win * Cin;
+      floatx4v acc[MTW];
+#pragma unroll
+      for (int t = 0; t < MTW; ++t) acc[t] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      // the row's whole A operand (all channels of this wave's pixels) in
+      // flight at once: one memory latency per (ky, iy) instead of one per
+      // 16-channel step
+      floatx4v a[MTW][12];
+#pragma unroll
+      for (int u = 0; u < 12; ++u)
+#pragma unroll
+        for (int t = 0; t < MTW; ++t) {
+          const int px = 16 * (w + NWV * t) + li;
+          a[t][u] = (u < U && px < Win) ? *(const floatx4v*)(xr + (size_t)px * Cin + 16 * u + 4 * lq)
+                                        : floatx4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+      for (int u = 0; u < 12; ++u) {
+        if (u < U) {
+          const floatx4v b4 = *(const floatx4v*)(wl + ((((kyi * U + u) * 4 + lq) * 16 + li) << 2));
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int t = 0; t < MTW; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u][v], b4[v], acc[t], 0, 0, 0);
+        }
+      }
+      // C/D map: row (pixel) 16*mtile + 4lq + r, col li
+#pragma unroll
+      for (int t = 0; t < MTW; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cm[(kyi * WMAX + 16 * (w + NWV * t) + 4 * lq + r) * 16 + li] = acc[t][r];
+    }
+    __syncthreads();
+    // gather, fixed order (ky ascending, kx ascending)
+    for (int X = tid; X < Wout; X += NT) {
+      float sum[4] = {0.f, 0.f, 0.f, 0.f};  // Cout <= 4 handled here (k*Cout <= 16)
+      for (int kyi = 0; kyi < nky; ++kyi) {
+        const int iy = (Y + pad - ky0 - 2 * kyi) >> 1;
+        if (iy < 0 || iy >= Hin) continue;
+        for (int kx = (X + pad) & 1; kx < k; kx += 2) {
+          const int ix = (X + pad - kx) >> 1;
+          if (ix < 0 || ix >= Win) continue;
+          const float* cp = cm + (kyi * WMAX + ix) * 16 + kx * Cout;
+          for (int o = 0; o < Cout; ++o) sum[o] += cp[o];
+        }
+      }
+      for (int o = 0; o < Cout; ++o) {
+        float v = sum[o] + (bias ? bias[o] : 0.f);
+        if (relu) v = v > 0.f ? v : 0.f;
+        y[n * ysn + o * ysc + (long long)Y * ysh + (long long)X * ysw] = v;
+      }
+    }
+  }
+}
 }  // namespace
 
 // y (NHWC, channel stride 1) = conv(x few-channel, wp [Cout][Kp] with k = t*C + c)
@@ -431,6 +542,33 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
   const int total = CG * Kc;
   hipLaunchKernelGGL(edge_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, grid, CG, Kc, C,
                      k * k, dw, db);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+// transposed conv 2x upsampling of a wide NHWC map to <= 4 channels (see tconv_few_kernel)
+bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, long long xsw, long long xsh,
+                  long long xsn, int Hin, int Win) {
+  return stride == 2 && k <= 5 && k >= 1 && Cout >= 1 && Cout <= 4 && k * Cout <= 16 && Cin % 16 == 0 &&
+         Cin <= 192 && Win <= 256 && xsc == 1 && xsw == Cin && xsh == (long long)Win * Cin &&
+         xsn == (long long)Hin * Win * Cin && pad >= 0;
+}
+
+int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float* W, int Cout, int k, int pad,
+                  const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
+                  int Hout, int Wout, hipStream_t s) {
+  if (((uintptr_t)x & 15) || Hout < 1 || Wout < 1) return IC_ERR_ARG;
+  const long long rows = (long long)N * ((Hout + 1) / 2);
+  long long grid = 2 * (rows < 256 ? rows : 256);  // two parities, <= 2 blocks per CU
+  if (Win <= 64)
+    hipLaunchKernelGGL((tconv_few_kernel<4, 1>), dim3((unsigned)grid), dim3(256), 0, s, x, N, Hin, Win, Cin, W, Cout,
+                       k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout);
+  else if (Win <= 128)
+    hipLaunchKernelGGL((tconv_few_kernel<8, 1>), dim3((unsigned)grid), dim3(512), 0, s, x, N, Hin, Win, Cin, W, Cout,
+                       k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout);
+  else
+    hipLaunchKernelGGL((tconv_few_kernel<8, 2>), dim3((unsigned)grid), dim3(512), 0, s, x, N, Hin, Win, Cin, W, Cout,
+                       k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }

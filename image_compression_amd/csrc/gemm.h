@@ -129,6 +129,11 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
 bool edge_wgrad_ok(int C, int k, int stride, long long sw, const float* G, int CG, long long gs_c, long long gs_w,
                    long long gs_h, long long gs_n, int Ho, int Wo);
 long long edge_units(int N, int Ho, int Wo);
+bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, long long xsw, long long xsh,
+                  long long xsn, int Hin, int Win);
+int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float* W, int Cout, int k, int pad,
+                  const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
+                  int Hout, int Wout, hipStream_t s);
 size_t edge_wgrad_ws(int CG, int Kc, long long units);
 int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
                    int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,

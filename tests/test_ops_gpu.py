@@ -70,6 +70,11 @@ TCONV_CASES = [
     (2, 192, 8, 8, 192, 5, 2, 2, 1),
     (2, 192, 4, 6, 192, 3, 1, 1, 0),   # h_s last layer form
     (2, 192, 16, 16, 3, 5, 2, 2, 1),   # last synthesis layer (Cout = 3, NCHW out)
+    (1, 64, 9, 7, 3, 5, 2, 2, 1),      # row-stationary few-channel kernel: ragged width
+    (1, 32, 3, 70, 3, 5, 2, 2, 1),     # 2 m-tiles per wave
+    (1, 16, 2, 130, 3, 3, 2, 1, 1),    # 4 m-tiles per wave, k = 3
+    (1, 48, 6, 5, 4, 3, 2, 1, 1),      # Cout = 4
+    (1, 32, 5, 5, 3, 5, 2, 2, 0),      # odd output height (no output padding)
     (1, 96, 5, 7, 64, 5, 2, 2, 1),
     (2, 320, 4, 4, 192, 5, 2, 2, 1),
 ]
