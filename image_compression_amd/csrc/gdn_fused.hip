@@ -446,20 +446,30 @@ __global__ void __launch_bounds__(512, 2)
 }
 
 // fixed-order sum of the per-block partials
-__global__ void gdn_slab_reduce_kernel(const float* __restrict__ slab, int nb, int C, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta) {
+// 64 elements x 4 groups of partials per block; each group sums a quarter of
+// the partials with eight loads in flight, the quarters combine in LDS in a
+// fixed order
+__global__ void __launch_bounds__(256) gdn_slab_reduce_kernel(const float* __restrict__ slab, int nb, int C,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float part[4][64];
   const int stride = C * C + C;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += gridDim.x * blockDim.x) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int b = 0;
-    for (; b + 3 < nb; b += 4) {
-      a0 += slab[(size_t)b * stride + i];
-      a1 += slab[(size_t)(b + 1) * stride + i];
-      a2 += slab[(size_t)(b + 2) * stride + i];
-      a3 += slab[(size_t)(b + 3) * stride + i];
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + e;
+  const int q = (nb + 3) >> 2, b0 = grp * q, b1 = min(nb, b0 + q);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < stride) {
+    const float* src = slab + i;
+    int b = b0;
+    for (; b + 7 < b1; b += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += src[(size_t)(b + j) * stride];
     }
-    for (; b < nb; ++b) a0 += slab[(size_t)b * stride + i];
-    const float v = (a0 + a1) + (a2 + a3);
+    for (int j = 0; b < b1; ++b, ++j) a[j] += src[(size_t)b * stride];
+  }
+  part[grp][e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (grp == 0 && i < stride) {
+    const float v = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
     if (i < C * C) {
       if (dgamma) dgamma[i] = v;
     } else if (dbeta) {
@@ -496,7 +506,7 @@ int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, con
                      (uint32_t)P);
   IC_CHECK_LAUNCH();
   const int stride = C * C + C;
-  hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 255) / 256), dim3(256), 0, s, slab, grid, C, dgamma,
+  hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
                      dbeta);
   IC_CHECK_LAUNCH();
   return IC_OK;
