@@ -238,6 +238,26 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   d.partial = part ? cv.take(part) : nullptr;
+  // fast layout: the phases' [t][n][r] packs are back to back in the
+  // workspace (each a multiple of 256 B), so one launch packs every phase
+  int ttot = 0;
+  bool contiguous = !d.generic;
+  for (int p = 0; p < np; ++p) {
+    ttot += d.ph[p].T;
+    contiguous = contiguous && wpb[p] % 256 == 0;
+  }
+  if (contiguous && ttot <= IC_MAXT) {
+    int aky[IC_MAXT], akx[IC_MAXT], t0 = 0;
+    for (int p = 0; p < np; ++p) {
+      float* wp = cv.take(wpb[p]);
+      d.ph[p].wp = wp;
+      for (int t = 0; t < d.ph[p].T; ++t) { aky[t0 + t] = pky[p][t]; akx[t0 + t] = pkx[p][t]; }
+      t0 += d.ph[p].T;
+    }
+    int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)d.ph[0].wp, s, d.bf16);
+    if (rc) return rc;
+    return ig_run(d, s);
+  }
   for (int p = 0; p < np; ++p) {
     float* wp = cv.take(wpb[p]);
     d.ph[p].wp = wp;
