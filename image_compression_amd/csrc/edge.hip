@@ -302,29 +302,38 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
       }
 }
 
-// fixed-order sum of the partials, scattered to dW[g][c][ky][kx] (+ db[g] from the ones column)
-__global__ void edge_wgrad_reduce_kernel(const float* __restrict__ slab, int nb, int CG, int Kc, int C, int T,
-                                         float* __restrict__ dw, float* __restrict__ db) {
+// fixed-order sum of the partials, scattered to dW[g][c][ky][kx] (+ db[g] from
+// the ones column): 64 elements x 4 groups of partials per block, eight loads
+// in flight per thread, the groups combined in LDS in a fixed order
+__global__ void __launch_bounds__(256) edge_wgrad_reduce_kernel(const float* __restrict__ slab, int nb, int CG, int Kc,
+                                                                int C, int T, float* __restrict__ dw,
+                                                                float* __restrict__ db) {
+  __shared__ float part[4][64];
   const int total = CG * Kc;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int gg = i / Kc, kk = i - (i / Kc) * Kc;
-    if (kk > T * C || (kk == T * C && !db)) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int b = 0;
-    for (; b + 3 < nb; b += 4) {
-      a0 += slab[(size_t)b * total + i];
-      a1 += slab[(size_t)(b + 1) * total + i];
-      a2 += slab[(size_t)(b + 2) * total + i];
-      a3 += slab[(size_t)(b + 3) * total + i];
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + e;
+  const int q = (nb + 3) >> 2, b0 = grp * q, b1 = min(nb, b0 + q);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    const float* src = slab + i;
+    int b = b0;
+    for (; b + 7 < b1; b += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += src[(size_t)(b + j) * total];
     }
-    for (; b < nb; ++b) a0 += slab[(size_t)b * total + i];
-    const float v = (a0 + a1) + (a2 + a3);
-    if (kk == T * C) {
-      db[gg] = v;
-    } else {
-      const int t = kk / C, c = kk - (kk / C) * C;
-      dw[((size_t)gg * C + c) * T + t] = v;
-    }
+    for (int j = 0; b < b1; ++b, ++j) a[j] += src[(size_t)b * total];
+  }
+  part[grp][e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (grp != 0 || i >= total) return;
+  const float v = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
+  const int gg = i / Kc, kk = i - (i / Kc) * Kc;
+  if (kk > T * C || (kk == T * C && !db)) return;
+  if (kk == T * C) {
+    db[gg] = v;
+  } else {
+    const int t = kk / C, c = kk - (kk / C) * C;
+    dw[((size_t)gg * C + c) * T + t] = v;
   }
 }
 
@@ -540,7 +549,7 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
 #undef EDGE_WG
   IC_CHECK_LAUNCH();
   const int total = CG * Kc;
-  hipLaunchKernelGGL(edge_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, grid, CG, Kc, C,
+  hipLaunchKernelGGL(edge_wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, slab, grid, CG, Kc, C,
                      k * k, dw, db);
   IC_CHECK_LAUNCH();
   return IC_OK;
