@@ -43,6 +43,19 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (__umulhi(n, f.m) + n) >> f.l;
 }
 
+// Exact three-term bf16 split of an fp32 value: a = h + m + l.  Each step
+// rounds to nearest even (v_cvt_pk_bf16_f32) and the residual a - h (then
+// minus m) is exact in fp32, so the three 8-bit significands carry all 24 of
+// a's.  Products of split operands are exact in fp32; keeping the six terms
+// h*h' + h*m' + m*h' + h*l' + m*m' + l*h' drops only terms below 2^-24 of the
+// product, i.e. the error of an fp32 fma chain.
+__device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)a;
+  const float r1 = a - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
 // 64-lane wave reduction (gfx950 wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -161,9 +161,11 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   P.Hg = y->h; P.Wg = y->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;
   d.Kc = d.generic ? (int)ic_align((size_t)P.T * x->c, 32) : x->c;
   d.bf16 = (math & IC_MATH_BF16) && !d.generic && x->c % 64 == 0 && aop == AOP_NONE;
+  d.x3 = (math & IC_MATH_SPLIT) && !d.bf16 && !d.generic && aop == AOP_NONE;
   const size_t part = ig_plan(d);
-  const size_t esz = d.bf16 ? 2 : 4;
+  const size_t esz = d.bf16 ? 2 : (d.x3 ? 6 : 4);
   const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * esz;
+  d.wplane = (long long)P.T * d.Npad * x->c;
   const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
   if (need) { *need = tot; return IC_OK; }
   if (wsb < tot) return IC_ERR_WORKSPACE;
@@ -171,7 +173,7 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   float* wp = cv.take(wpb);
   d.partial = part ? cv.take(part) : nullptr;
   P.wp = wp;
-  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.bf16);
+  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.x3 ? 2 : d.bf16);
   if (rc) return rc;
   return ig_run(d, s);
 }
@@ -227,7 +229,30 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   d.nphase = np;
   d.Kc = d.generic ? (int)ic_align((size_t)tmax * x->c, 32) : x->c;
   d.bf16 = (math & IC_MATH_BF16) && !d.generic && x->c % 64 == 0;
+  int ttot = 0;
+  for (int p = 0; p < np; ++p) ttot += d.ph[p].T;
+  d.x3 = (math & IC_MATH_SPLIT) && !d.bf16 && !d.generic && ttot <= IC_MAXT;
   const size_t part = ig_plan(d);
+  if (d.x3) {
+    // one pack of three bf16 planes [part][t over all phases][Npad][Cin]
+    d.wplane = (long long)ttot * d.Npad * x->c;
+    const size_t wb = (size_t)d.wplane * 6;
+    const size_t tot = ic_align(part, 256) + ic_align(wb, 256);
+    if (need) { *need = tot; return IC_OK; }
+    if (wsb < tot) return IC_ERR_WORKSPACE;
+    Carve cv{(char*)ws, 0};
+    d.partial = part ? cv.take(part) : nullptr;
+    __bf16* base = (__bf16*)cv.take(wb);
+    int aky[IC_MAXT], akx[IC_MAXT], t0 = 0;
+    for (int p = 0; p < np; ++p) {
+      d.ph[p].wp = (const float*)(base + (size_t)t0 * d.Npad * x->c);
+      for (int t = 0; t < d.ph[p].T; ++t) { aky[t0 + t] = pky[p][t]; akx[t0 + t] = pkx[p][t]; }
+      t0 += d.ph[p].T;
+    }
+    int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)base, s, 2);
+    if (rc) return rc;
+    return ig_run(d, s);
+  }
   size_t wpb[IC_MAXPH];
   size_t tot = ic_align(part, 256);
   for (int p = 0; p < np; ++p) {
@@ -240,12 +265,8 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   d.partial = part ? cv.take(part) : nullptr;
   // fast layout: the phases' [t][n][r] packs are back to back in the
   // workspace (each a multiple of 256 B), so one launch packs every phase
-  int ttot = 0;
   bool contiguous = !d.generic;
-  for (int p = 0; p < np; ++p) {
-    ttot += d.ph[p].T;
-    contiguous = contiguous && wpb[p] % 256 == 0;
-  }
+  for (int p = 0; p < np; ++p) contiguous = contiguous && wpb[p] % 256 == 0;
   if (contiguous && ttot <= IC_MAXT) {
     int aky[IC_MAXT], akx[IC_MAXT], t0 = 0;
     for (int p = 0; p < np; ++p) {

@@ -54,6 +54,9 @@ struct IgDesc {
   long long Mtot;
   int bm, bn;        // chosen tile (set by ig_plan)
   int bf16;          // bf16 operands, fp32 accumulation (fast path, Cin % 64 == 0); wp holds bf16
+  int x3;            // fp32 by exact three-term bf16 split (fast path, Cin % 32 == 0); wp holds three
+                     // bf16 planes [part][t][Npad][Cin], part p at wp + p * wplane (bf16 elements)
+  long long wplane;
   IgPhase ph[IC_MAXPH];
 };
 
@@ -102,7 +105,9 @@ int colsum(const float* t, long long s_n, long long s_c, long long s_h, long lon
 //  mode 2 (scatter):    wp[0][t*B + b][a] = W[a][b][ky_t][kx_t]   (rows n >= T*B zero)
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic,
                  int T, const int* ky, const int* kx, int Npad, int Kpad,
-                 float* wp, hipStream_t s, int out_bf16 = 0);  // out_bf16: wp is __bf16[]
+                 float* wp, hipStream_t s, int out_bf16 = 0);
+// out_bf16: 1 -> wp is __bf16[] (rounded); 2 -> wp is three __bf16 planes (exact split
+// w = w0 + w1 + w2, plane stride = the pack's element count)
 
 // few-channel edges (im2col.hip)
 int im2col_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H,

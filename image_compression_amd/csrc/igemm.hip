@@ -406,6 +406,157 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
   ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
 }
 
+// ------------------------------------------------------------------ fp32 by exact bf16 split
+// The fp32 implicit GEMM on the bf16 MFMA: every fp32 operand is split exactly
+// into three bf16 terms (split3_bf16), and the six cross products that carry
+// the product down to 2^-24 of its size are accumulated in fp32 on
+// v_mfma_f32_32x32x16_bf16 (1/16 the cycles of the fp32 MFMA per product, so
+// six of them cost 3/8 of v_mfma_f32_32x32x2_f32's time per MAC).  The error
+// is that of an fp32 fma chain (tests/test_ops_gpu.py pins it against the
+// fp64 oracle beside the native fp32 kernel).  Activations are read as fp32
+// and split on their way into LDS; weights arrive as three pre-split bf16
+// planes.  K chunk = 32 channels of one tap (Cin % 32 == 0), channel-chunk
+// outer / tap inner as in ig_kernel; LDS rows of 40 bf16 (80 B) keep the
+// 16-B fragment reads of 16 consecutive rows on distinct banks.
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
+  constexpr int LDB = 40;
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int APASS = BM / 32, BPASS = BN / 64;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(BN % 64 == 0, "B staged 64 rows per pass");
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * BM * LDB];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * BN * LDB];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = P.T * (d.Cin >> 5);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x;
+  const int lrow = tid >> 3, lc4 = tid & 7;   // A: 8 float4 per 32-channel row
+  const int brow = tid >> 2, bq = tid & 3;    // B: 4 x 16 B per 32-wide bf16 row
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[APASS];
+  int a_iy[APASS], a_ix[APASS];
+#pragma unroll
+  for (int p = 0; p < APASS; ++p) {
+    const uint32_t m = m0 + lrow + 32 * p;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[p] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[p] = (int)gx * d.stride;
+    a_off[p] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[p] * xsh + (uint32_t)a_ix[p] * xsw;
+  }
+  const float* __restrict__ xg = d.x;
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  const size_t wplane = (size_t)d.wplane;
+
+  floatx4v ra[APASS];
+  bf16x8 rb[3][BPASS];
+  auto gload = [&](int c) {
+    const int cc = c / P.T, t = c - cc * P.T;
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+      const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;
+      ra[p] = *(const floatx4v*)src;
+    }
+    const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 32 + bq * 8;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int p = 0; p < BPASS; ++p) rb[q][p] = *(const bf16x8*)(wb + q * wplane + (size_t)(64 * p) * d.Cin);
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+      bf16x4 vh, vm, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 h, m, l;
+        split3_bf16(ra[p][e], h, m, l);
+        vh[e] = h; vm[e] = m; vl[e] = l;
+      }
+      __bf16* dst = &As[(lrow + 32 * p) * LDB + lc4 * 4];
+      *(bf16x4*)dst = vh;
+      *(bf16x4*)(dst + BM * LDB) = vm;
+      *(bf16x4*)(dst + 2 * BM * LDB) = vl;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[(q * BN + brow + 64 * p) * LDB + bq * 8] = rb[q][p];
+  };
+
+  const int lane = tid & 63, w = tid >> 6;
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 31, h = lane >> 5;
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (cb < ce) {
+    gload(cb);
+    sstore();
+  }
+  __syncthreads();
+  const __bf16* Ard = &As[(wm * WM + r) * LDB + 8 * h];
+  const __bf16* Brd = &Bs[(wn * WN + r) * LDB + 8 * h];
+  for (int c = cb; c < ce; ++c) {
+    if (c + 1 < ce) gload(c + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 32) * LDB + 16 * s);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(Brd + (q * BN + j * 32) * LDB + 16 * s);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          // small terms first, the leading product last
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (c + 1 < ce) sstore();
+    __syncthreads();
+  }
+  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
+}
+
 // split-K reduction + epilogue: one thread per (row, channel)
 __global__ void ig_reduce_kernel(const IgDesc d) {
   const long long total = d.Mtot * d.Cout;
@@ -444,6 +595,13 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   if (d.bf16) {
     if (sq) return IC_ERR_ARG;
     hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+  } else if (d.x3) {
+    if constexpr (BN % 64 == 0) {
+      if (sq) return IC_ERR_ARG;
+      hipLaunchKernelGGL((ig_kernel_x3<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+    } else {
+      return IC_ERR_ARG;
+    }
   } else if (d.generic) {
     if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
@@ -478,6 +636,7 @@ size_t ig_plan(IgDesc& d) {
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
   else { d.bm = 256; d.bn = 32; }
+  if (d.bn % 64 != 0) d.x3 = 0;  // the split kernel stages B 64 rows per pass; native fp32 instead
   d.Npad = ig_npad(d.Cout);
   long long mtot = 0;
   long long tiles = 0;
@@ -518,6 +677,7 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.Mtot == 0) return IC_OK;
   if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
   if (d.bf16 && (d.generic || d.Cin % 64 != 0)) return IC_ERR_ARG;
+  if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op != AOP_NONE || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
   if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);

@@ -15,6 +15,21 @@ struct PackArgs {
   int ky[IC_MAXT], kx[IC_MAXT];
 };
 
+__device__ __forceinline__ void store_packed(const PackArgs& p, long long i, long long total, float v) {
+  if (p.out_bf16 == 2) {  // three planes of the exact split, plane stride = total
+    __bf16 h, m, l;
+    split3_bf16(v, h, m, l);
+    __bf16* o = (__bf16*)p.wp;
+    o[i] = h;
+    o[i + total] = m;
+    o[i + 2 * total] = l;
+  } else if (p.out_bf16) {
+    ((__bf16*)p.wp)[i] = (__bf16)v;  // round to nearest even
+  } else {
+    p.wp[i] = v;
+  }
+}
+
 __global__ void pack_kernel(const PackArgs p) {
   const int Nout = p.mode == 0 ? p.A : p.B;
   const int R = p.mode == 0 ? p.B : p.A;
@@ -41,8 +56,7 @@ __global__ void pack_kernel(const PackArgs p) {
       const int nn = (int)(i / p.A);
       const int tt = nn / p.B, b = nn - (nn / p.B) * p.B;
       if (tt < p.T) v = p.W[(((long long)a * p.B + b) * p.k + p.ky[tt]) * p.k + p.kx[tt]];
-      if (p.out_bf16) ((__bf16*)p.wp)[i] = (__bf16)v;
-      else p.wp[i] = v;
+      store_packed(p, i, total, v);
       continue;
     }
     if (n < Nout && t < p.T) {
@@ -50,8 +64,7 @@ __global__ void pack_kernel(const PackArgs p) {
       const int b = p.mode == 0 ? r : n;
       v = p.W[(((long long)a * p.B + b) * p.k + p.ky[t]) * p.k + p.kx[t]];
     }
-    if (p.out_bf16) ((__bf16*)p.wp)[i] = (__bf16)v;  // round to nearest even
-    else p.wp[i] = v;
+    store_packed(p, i, total, v);
   }
 }
 }  // namespace

@@ -187,11 +187,15 @@ class ConvTranspose2dFn(Function):
         return dx, dw, db, None, None, None, None, None
 
 
-MATH = {"fp32": 0, "bf16": 1}   # include/imgcomp.h IC_MATH_*
+# include/imgcomp.h IC_MATH_*: "fp32" exact fp32 MFMA; "bf16" bf16 operands, fp32 accumulation
+# (reduced precision, config C3); "fp32_split" fp32 arithmetic on the bf16 MFMA through an exact
+# three-term bf16 split of both operands (six products, error of an fp32 fma chain)
+MATH = {"fp32": 0, "bf16": 1, "fp32_split": 2}
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, act=0, math=0):
-    """`math`: 0 fp32 (default), 1 bf16 operands with fp32 accumulation (fwd and dgrad)."""
+    """`math` (forward and input gradient): 0 fp32 (default), 1 bf16 operands with fp32
+    accumulation, 2 fp32 by exact bf16 split (see MATH)."""
     return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), int(act), int(math))
 
 

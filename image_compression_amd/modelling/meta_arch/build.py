@@ -5,25 +5,35 @@ META_ARCH_REGISTRY = Registry("META_ARCH")
 
 def build_model(cfg):
     """cfg.MODEL.META_ARCHITECTURE -> nn.Module (reference meta_arch/build.py:30-36).
-    cfg.MODEL.COMPUTE_DTYPE ("fp32" default, or "bf16": BASELINE config C3) is
-    this build's addition; see set_compute_dtype."""
+    cfg.MODEL.COMPUTE_DTYPE ("fp32" default, "fp32_split", or "bf16": BASELINE
+    config C3) is this build's addition; see set_compute_dtype."""
     model = META_ARCH_REGISTRY.get(cfg.MODEL.META_ARCHITECTURE)(cfg)
     set_compute_dtype(model, cfg.MODEL.get("COMPUTE_DTYPE", "fp32"))
     return model
 
 
 def set_compute_dtype(model, dtype):
-    """Operand precision of the main transforms' (g_a, g_s) wide convolution
-    forward / input-gradient GEMMs: "fp32" (exact fp32 MFMA) or "bf16" (bf16
-    operands, fp32 accumulation) — 97 % of the model's FLOPs.  The
-    hyperprior transforms (h_a, h_s: 1.3 % of the FLOPs, but they shape the
-    rate term's gradients), weight gradients, GDN, the entropy models and the
-    3-channel image edges always compute in fp32."""
+    """Arithmetic of the wide convolution forward / input-gradient GEMMs.
+    "fp32": the fp32 MFMA (an exact fp32 fma chain).  "fp32_split": fp32
+    arithmetic on the bf16 MFMA — both operands split exactly into three bf16
+    terms, six cross products accumulated in fp32, error of an fp32 fma chain
+    (functional.MATH) — on every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16
+    operands with fp32 accumulation (reduced precision, BASELINE config C3) on
+    the main transforms (g_a, g_s) only — 97 % of the model's FLOPs; the
+    hyperprior transforms (1.3 % of the FLOPs, but they shape the rate term's
+    gradients) stay fp32.  Weight gradients, GDN, the entropy models and the
+    3-channel image edges compute in fp32 in every mode."""
     from ...functional import MATH
     from ..layers.conv import Conv2d, ConvTranspose2d
     if dtype not in MATH:
         raise ValueError(f"compute dtype {dtype!r}: expected one of {sorted(MATH)}")
-    for name in ("analysis_transform", "synthesis_transform"):
+    subs = ("analysis_transform", "synthesis_transform")
+    if dtype == "fp32_split":
+        subs += ("prior_analysis", "prior_synthesis")
+    for m in model.modules():
+        if isinstance(m, (Conv2d, ConvTranspose2d)):
+            m.math = 0
+    for name in subs:
         sub = getattr(model, name, None)
         if sub is None:
             continue

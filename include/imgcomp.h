@@ -90,6 +90,11 @@ int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stri
  *      and all weight gradients / GDN stay fp32. */
 #define IC_MATH_FP32 0
 #define IC_MATH_BF16 1
+/*      IC_MATH_SPLIT: fp32 arithmetic on the bf16 MFMA — each fp32 operand split exactly into
+ *      three bf16 terms, six cross products accumulated in fp32 (error of an fp32 fma chain,
+ *      3/8 of the native fp32 MFMA's cycles per MAC); layers with reduction channels % 32 == 0
+ *      and >= 64 output channels, others run the native fp32 kernel. */
+#define IC_MATH_SPLIT 2
 size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
 int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
                      const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="run only ops whose 'layer op' contains this text")
+    ap.add_argument("--math", type=int, default=0, help="IC_MATH_* of the conv fwd / dgrad (0 fp32, 2 fp32 split)")
     a = ap.parse_args()
     global ONLY
     ONLY = a.only
@@ -83,6 +84,13 @@ def main():
         fwd, fws = getattr(L, pref + "_fwd"), getattr(L, pref + "_fwd_ws")
         dg, dgws = getattr(L, pref + "_dgrad"), getattr(L, pref + "_dgrad_ws")
         wg, wgws = getattr(L, pref + "_wgrad"), getattr(L, pref + "_wgrad_ws")
+        if a.math:
+            fwd_ex, fws_ex = getattr(L, pref + "_fwd_ex"), getattr(L, pref + "_fwd_ws_ex")
+            dg_ex, dgws_ex = getattr(L, pref + "_dgrad_ex"), getattr(L, pref + "_dgrad_ws_ex")
+            fws = lambda *q: fws_ex(*q, a.math)  # noqa: E731
+            fwd = lambda *q: fwd_ex(*q[:8], a.math, *q[8:])  # noqa: E731
+            dgws = lambda *q: dgws_ex(*q, a.math)  # noqa: E731
+            dg = lambda *q: dg_ex(*q[:6], a.math, *q[6:])  # noqa: E731
         n1 = fws(ax, k, s, p, ay)
         b1 = ws(n1)
         ms = t_ms(lambda: _lib.check(fwd(ax, _lib.ptr(w), _lib.ptr(b), k, s, p, ay, 0, _lib.ptr(b1), n1, st), "fwd"), a.reps, name + " fwd")
