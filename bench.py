@@ -38,16 +38,31 @@ METRIC = "256x256 images/s fwd+bwd at 1/2/4/8 GPUs; bpp & PSNR vs ref on Kodak"
 # default; the others select the same path at their own lambda / loss / width /
 # precision / size (per-GPU batch for weak scaling; C4 = 64 over 4 GPUs, C5 =
 # 128 over 8 GPUs).
+# `math` is cfg.MODEL.COMPUTE_DTYPE: "fp32_split" = fp32 arithmetic on the bf16 MFMA (each
+# fp32 operand split exactly into three bf16 terms, six cross products accumulated in fp32:
+# the error of an fp32 fma chain, tests/test_split_gpu.py), "fp32" = the fp32 MFMA,
+# "bf16" = bf16 operands (C3's reduced precision).
 CONFIGS = {
     "C2": dict(desc="psnr_256 (lambda=256, MSE, Laplacian conditional, 192/192 ch), fp32",
-               lam=256.0, loss=["MSE"], latent=192, dtype="fp32", batch=32, size=256, gflop=73.70),
+               lam=256.0, loss=["MSE"], latent=192, dtype="fp32", math="fp32_split", batch=32, size=256,
+               gflop=73.70),
     "C3": dict(desc="psnr_4096 (lambda=4096, MSE, latent 320), bf16 operands / fp32 accumulation",
-               lam=4096.0, loss=["MSE"], latent=320, dtype="bf16", batch=32, size=256, gflop=76.27),
+               lam=4096.0, loss=["MSE"], latent=320, dtype="bf16", math="bf16", batch=32, size=256, gflop=76.27),
     "C4": dict(desc="ssim_64 (lambda=64, MS-SSIM log-scale loss), fp32",
-               lam=64.0, loss=["MS_SSIMLoss"], latent=192, dtype="fp32", batch=16, size=256, gflop=74.55),
+               lam=64.0, loss=["MS_SSIMLoss"], latent=192, dtype="fp32", math="fp32_split", batch=16, size=256,
+               gflop=74.55),
     "C5": dict(desc="psnr_8192 (lambda=8192, MSE), 512x512 crops, fp32",
-               lam=8192.0, loss=["MSE"], latent=192, dtype="fp32", batch=16, size=512, gflop=73.70),
+               lam=8192.0, loss=["MSE"], latent=192, dtype="fp32", math="fp32_split", batch=16, size=512,
+               gflop=73.70),
 }
+MATH_NOTE = {
+    "fp32_split": "fp32 via exact 3-term bf16 operand split, 6 products on v_mfma_f32_32x32x16_bf16, fp32 "
+                  "accumulation (fp32 fma-chain error; wide conv fwd/dgrad); weight gradients, GDN, entropy "
+                  "models, edges on the fp32 MFMA / VALU",
+    "fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain)",
+    "bf16": "bf16 operands, fp32 accumulation (g_a/g_s conv fwd/dgrad); rest fp32",
+}
+BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
 
 
 def _cfg(lam=256.0, conf=None):
@@ -60,11 +75,11 @@ def _cfg(lam=256.0, conf=None):
         cfg.MODEL.LOSS.DISTORTION_LOSS_NAMES = list(conf["loss"])
         cfg.MODEL.LOSS.SSIM.LOG_SCALE = True      # the ssim_* configs
         cfg.MODEL.LATENT_CHANNELS = conf["latent"]
-        cfg.MODEL.COMPUTE_DTYPE = conf["dtype"]
+        cfg.MODEL.COMPUTE_DTYPE = conf["math"]
     return cfg
 
 
-def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0):
+def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="fp32"):
     """The implicit-GEMM conv kernel on g_a layer 2 (conv 5x5 s2, 192->192,
     128x128 -> 64x64, batch 32): one launch = 2 * (32*64*64) * 192 * (25*192)
     = 241.6 GFLOP of algorithmic work.  `live_ms` is its average duration
@@ -78,21 +93,29 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0):
     flop = 2.0 * (32 * 64 * 64) * 192 * (25 * 192)
     with torch.no_grad():
         for _ in range(3):
-            IF.conv2d(x, w, b, 2, 2)
+            IF.conv2d(x, w, b, 2, 2, math=IF.MATH[math])
         torch.cuda.synchronize()
         st = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(reps):
-            IF.conv2d(x, w, b, 2, 2)
+            IF.conv2d(x, w, b, 2, 2, math=IF.MATH[math])
         e1.record(st)
         torch.cuda.synchronize()
     iso_ms = e0.elapsed_time(e1) / reps
     ms = live_ms if live_ms else iso_ms
     achieved = flop / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": _pmc_traffic(),
-            "kernel": "ig_kernel<128,192,64,96> + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
+    if math == "fp32_split":
+        # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
+        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3<128,192,64,96> (fp32 by 3-term bf16 split)"
+    else:
+        peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(kern.split(" ")[0]),
+            "peak_note": ("algorithmic fp32 FLOP/s; peak = bf16 dense MFMA 2500 TF / 6 products per fp32 MAC"
+                          if math == "fp32_split" else "fp32 dense MFMA spec"),
+            "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "kernel": kern + " + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4),
             "timing": (f"live: HIP events on the launch stream around the layer's {live_launches} launches "
                        "inside the timed steps" if live_ms else "isolated loop of the same launch"),
@@ -160,17 +183,18 @@ def optimizer_step_ms(model, dev, reps=20):
     return round(e0.elapsed_time(e1) / reps, 4)
 
 
-def _pmc_traffic():
+def _pmc_traffic(kernel):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC passes (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/*_pmc_dominant.json):
     FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE.  The algorithmic bytes of
     the launch are 0.51 GB (input 403 MB, weights 3.7 MB, output 101 MB)."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_dominant.json")))
-    if not files:
-        return None
-    with open(files[-1]) as fh:
-        return round(json.load(fh)["traffic_bytes_per_launch"])
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_dominant.json")), reverse=True):
+        with open(f) as fh:
+            rec = json.load(fh)
+        if rec["kernel"].split("<")[0] == kernel.split("<")[0]:
+            return round(rec["traffic_bytes_per_launch"])
+    return None
 
 
 def _mfma_peak_measured():
@@ -231,8 +255,12 @@ def main():
                          "after the replay) instead of eager launches (N > 1: DDP, 12 MB buckets "
                          "overlapped with the backward).  Measured equal at N=1: the GPU, not the host, "
                          "paces the launches.")
+    ap.add_argument("--math", default=None, choices=["fp32", "fp32_split", "bf16"],
+                    help="override the config's cfg.MODEL.COMPUTE_DTYPE")
     args = ap.parse_args()
-    conf = CONFIGS[args.config]
+    conf = dict(CONFIGS[args.config])
+    if args.math:
+        conf["math"] = args.math
     args.batch = args.batch or conf["batch"]
     args.size = args.size or conf["size"]
 
@@ -296,7 +324,7 @@ def main():
     roof = None
     if not args.no_roofline and args.config == "C2":
         roof = dominant_kernel_roofline(dev, live_ms=live.ms() if live else None,
-                                        live_launches=len(live.pairs) if live else 0)
+                                        live_launches=len(live.pairs) if live else 0, math=conf["math"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline()
@@ -312,6 +340,7 @@ def main():
             "config": {"workload": f"{args.config}: {conf['desc']}, "
                                    f"{args.size}x{args.size}, {args.batch} images/GPU, fwd+loss+bwd"
                                    + (" + grad all-reduce" if dist else "") + f" [{mode}]",
+                       "math": f"{conf['math']}: {MATH_NOTE[conf['math']]}",
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(step_tflops, 2),

@@ -11,6 +11,16 @@
 // per chunk are contiguous in LDS -> 4 x ds_read_b128 per operand tile.
 #include "gemm.h"
 
+#ifndef IG_X3_REG
+#define IG_X3_REG 1  // 1: register-staged split kernel (ig_kernel_x3); 0: the LDS-DMA one (ig_kernel_x3d, measured slower)
+#endif
+#ifndef IG_X3_NST
+#define IG_X3_NST 3  // LDS stages of the LDS-DMA split kernel
+#endif
+#ifndef IG_X3_ABL
+#define IG_X3_ABL 0  // ablation builds (tools/abl_build.sh): 1 no weight reloads, 2 no activation reloads, 3 no MFMA
+#endif
+
 namespace {
 
 constexpr int LDK = 36;
@@ -473,6 +483,9 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
     const int cc = c / P.T, t = c - cc * P.T;
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
+#if IG_X3_ABL == 2
+    if (c == cb)
+#endif
 #pragma unroll
     for (int p = 0; p < APASS; ++p) {
       const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
@@ -481,6 +494,9 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
       ra[p] = *(const floatx4v*)src;
     }
     const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 32 + bq * 8;
+#if IG_X3_ABL == 1
+    if (c == cb)
+#endif
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -541,6 +557,10 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+#if IG_X3_ABL == 3
+          if (acc[i][j][0] == 12345.f) acc[i][j] += (floatx16)(float)(a[0][i][0] + a[1][i][1] + a[2][i][2] + b[0][j][0] + b[1][j][1] + b[2][j][2]);
+          continue;
+#endif
           // small terms first, the leading product last
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
@@ -553,6 +573,190 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
     __syncthreads();
     if (c + 1 < ce) sstore();
     __syncthreads();
+  }
+  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
+}
+
+// ------------------------------------------------------------------ split, LDS-DMA staged
+// Same arithmetic as ig_kernel_x3, staged without a VGPR round trip: each
+// 16-channel K chunk (one tap) arrives by LDS-DMA (global_load_lds_dwordx4)
+// into an NST-deep ring of LDS stages, chunk c + NST - 1 in flight while chunk
+// c computes, one barrier per chunk.  The activations land as fp32 and are
+// split into their three bf16 terms in registers as the A fragments are read;
+// the weights land as the three pre-split bf16 planes.  LDS-DMA writes its
+// 64 lanes' 16-B pieces lane-linearly, so the bank swizzles are applied on the
+// DMA source side:
+//   A stage [BM rows][4 x 16-B chunks of fp32]: chunk c of row r at c ^ ((r >> 2) & 3)
+//   B plane [BN rows][2 x 16-B chunks of bf16]: chunk c of row n at c ^ ((n >> 3) & 1)
+// which keeps every 16-lane group of the ds_read_b128 fragment reads on
+// distinct banks (MI355X_MICROARCH.md §LDS lane groups).
+typedef __attribute__((address_space(3))) void* ig_lds_t;
+typedef const __attribute__((address_space(1))) void* ig_gbl_t;
+
+// DMA instructions wave w issues per stage, and a counted wait that leaves
+// the later stages' DMAs in flight
+constexpr int ig_cntw(int ins, int pw, int w) {
+  int n = 0;
+  for (int j = 0; j < pw; ++j) n += (4 * j + w < ins) ? 1 : 0;
+  return n;
+}
+template <int N>
+__device__ __forceinline__ void ig_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int NST>
+__global__ void __launch_bounds__(256, 2) ig_kernel_x3d(const IgDesc d) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int A_BYTES = BM * 64;
+  constexpr int B_PLANE = BN * 32;
+  constexpr int STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int A_INS = A_BYTES / 1024, B_INS = 3 * B_PLANE / 1024;  // 1-KB wave DMA instructions per stage
+  constexpr int A_PW = (A_INS + 3) / 4, B_PW = (B_INS + 3) / 4;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "whole DMA instructions");
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = P.T * (d.Cin >> 4);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  const float* __restrict__ xg = d.x;
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+
+  // per DMA instruction j of this wave: the row (pixel) it feeds and its channel offset
+  uint32_t a_off[A_PW];
+  int a_iy[A_PW], a_ix[A_PW];
+#pragma unroll
+  for (int j = 0; j < A_PW; ++j) {
+    const int g = j * 4 + w;
+    const int o = g * 1024 + lane * 16;
+    const int r = o >> 6, cp = (o >> 4) & 3;
+    const int c = cp ^ ((r >> 2) & 3);
+    const uint32_t m = m0 + r;
+    const bool ok = g < A_INS && m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[j] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[j] = (int)gx * d.stride;
+    a_off[j] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[j] * xsh + (uint32_t)a_ix[j] * xsw + (uint32_t)(c * 4);
+  }
+  uint32_t b_off[B_PW];
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    const int g = j * 4 + w;
+    const int o = g * 1024 + lane * 16;
+    const int q = o / B_PLANE, rem = o - q * B_PLANE;
+    const int n = rem >> 5, cp = (rem >> 4) & 1;
+    const int c = cp ^ ((n >> 3) & 1);
+    b_off[j] = (uint32_t)(q * d.wplane) + (uint32_t)(n0 + n) * (uint32_t)d.Cin + (uint32_t)(c * 8);
+  }
+  const uint32_t tstride = (uint32_t)d.Npad * (uint32_t)d.Cin;
+
+  auto stage = [&](int c, int buf) {
+    const int cc = c / P.T, t = c - cc * P.T;
+    const int dy = P.dy[t], dx = P.dx[t];
+    char* base = lds + buf * STAGE;
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 16);
+#pragma unroll
+    for (int j = 0; j < A_PW; ++j) {
+      if (j * 4 + w < A_INS) {  // wave-uniform
+        const int iy = a_iy[j] + dy, ix = a_ix[j] + dx;
+        const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+        const float* src = in ? xg + (a_off[j] + toff) : ig_zero_page;
+        __builtin_amdgcn_global_load_lds((ig_gbl_t)src, (ig_lds_t)(base + (j * 4 + w) * 1024), 16, 0, 0);
+      }
+    }
+    const uint32_t woff = (uint32_t)t * tstride + (uint32_t)(cc * 16);
+#pragma unroll
+    for (int j = 0; j < B_PW; ++j) {
+      if (j * 4 + w < B_INS)
+        __builtin_amdgcn_global_load_lds((ig_gbl_t)(wpb + (b_off[j] + woff)),
+                                         (ig_lds_t)(base + A_BYTES + (j * 4 + w) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 31, h = lane >> 5;
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // fragment byte offsets inside a stage (row bits above 4 do not change the swizzles)
+  const int sa = (r >> 2) & 3;
+  const int a_rd0 = (wm * WM + r) * 64 + 16 * ((2 * h) ^ sa);
+  const int a_rd1 = (wm * WM + r) * 64 + 16 * ((2 * h + 1) ^ sa);
+  const int b_rd = A_BYTES + (wn * WN + r) * 32 + 16 * (h ^ ((r >> 3) & 1));
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (cb + s < ce) stage(cb + s, s);
+  int buf = 0;
+  for (int c = cb; c < ce; ++c) {
+    // own DMAs of chunk c have landed (those of the NST-2 later chunks may still fly), then barrier
+    if (NST > 2 && c + 1 < ce) {
+      switch (w) {
+        case 0: ig_vm_wait<ig_cntw(A_INS, A_PW, 0) + ig_cntw(B_INS, B_PW, 0)>(); break;
+        case 1: ig_vm_wait<ig_cntw(A_INS, A_PW, 1) + ig_cntw(B_INS, B_PW, 1)>(); break;
+        case 2: ig_vm_wait<ig_cntw(A_INS, A_PW, 2) + ig_cntw(B_INS, B_PW, 2)>(); break;
+        default: ig_vm_wait<ig_cntw(A_INS, A_PW, 3) + ig_cntw(B_INS, B_PW, 3)>(); break;
+      }
+    } else {
+      ig_vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (c + NST - 1 < ce) stage(c + NST - 1, (buf + NST - 1) % NST);
+    const char* sb = lds + buf * STAGE;
+    bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const floatx4v v0 = *(const floatx4v*)(sb + a_rd0 + i * 32 * 64);
+      const floatx4v v1 = *(const floatx4v*)(sb + a_rd1 + i * 32 * 64);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 hh, mm, ll;
+        split3_bf16(e < 4 ? v0[e] : v1[e - 4], hh, mm, ll);
+        a[0][i][e] = hh; a[1][i][e] = mm; a[2][i][e] = ll;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(sb + b_rd + q * B_PLANE + j * 32 * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+    buf = buf + 1 == NST ? 0 : buf + 1;
   }
   ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
 }
@@ -598,7 +802,11 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   } else if (d.x3) {
     if constexpr (BN % 64 == 0) {
       if (sq) return IC_ERR_ARG;
+#if IG_X3_REG
       hipLaunchKernelGGL((ig_kernel_x3<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+#else
+      hipLaunchKernelGGL((ig_kernel_x3d<BM, BN, WM, WN, IG_X3_NST>), grid, dim3(256), 0, s, d);
+#endif
     } else {
       return IC_ERR_ARG;
     }
@@ -650,7 +858,8 @@ size_t ig_plan(IgDesc& d) {
     P.m_off = mtot;
     mtot += M;
     tiles += (long long)P.mtiles * (d.Npad / d.bn);
-    const int nch = d.generic ? (d.Kc >> 5) : P.T * (d.bf16 ? (d.Cin >> 6) : (d.Cin >> 5));
+    const int nch = d.generic ? (d.Kc >> 5)
+                  : P.T * (d.bf16 ? (d.Cin >> 6) : (d.x3 && !IG_X3_REG) ? (d.Cin >> 4) : (d.Cin >> 5));
     nchunks_max = nch > nchunks_max ? nch : nchunks_max;
   }
   d.Mtot = mtot;

@@ -16,7 +16,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "ig_kernel<128, 192, 64, 96, false, false>"
+KERNEL = os.environ.get("PMC_KERNEL", "ig_kernel<128, 192, 64, 96, false, false>")
 
 
 def _values(path, counter):
