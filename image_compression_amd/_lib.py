@@ -69,6 +69,11 @@ SIGNATURES = {
     "ic_conv_transpose2d_dgrad": (c_int, [_ACT, c_void, c_int, c_int, c_int, _ACT, c_void, c_size, c_void]),
     "ic_conv_transpose2d_wgrad_ws": (c_size, [_ACT, _ACT, c_int, c_int, c_int]),
     "ic_conv_transpose2d_wgrad": (c_int, [_ACT, _ACT, c_int, c_int, c_int, c_void, c_void, c_void, c_size, c_void]),
+    "ic_conv2d_wgrad_ws_ex": (c_size, [_ACT, _ACT, c_int, c_int, c_int, c_int]),
+    "ic_conv2d_wgrad_ex": (c_int, [_ACT, _ACT, c_int, c_int, c_int, c_void, c_void, c_int, c_void, c_size, c_void]),
+    "ic_conv_transpose2d_wgrad_ws_ex": (c_size, [_ACT, _ACT, c_int, c_int, c_int, c_int]),
+    "ic_conv_transpose2d_wgrad_ex": (c_int, [_ACT, _ACT, c_int, c_int, c_int, c_void, c_void, c_int, c_void, c_size,
+                                             c_void]),
     "ic_gdn_fwd_ws": (c_size, [_ACT]),
     "ic_gdn_fwd": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_void, c_size, c_void]),
     "ic_gdn_bwd_ws": (c_size, [_ACT]),

@@ -290,7 +290,7 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
 
 // dW[g][c][ky][kx] = sum_p G[p][g] * X[p*s + ky - pad][c]; db = colsum(bias_src)
 int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, float* dw,
-               const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+               const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (G->n != X->n) return IC_ERR_ARG;
   if ((X->h + 2 * pad - k) / stride + 1 != G->h || (X->w + 2 * pad - k) / stride + 1 != G->w)
@@ -302,6 +302,7 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   d.Hx = X->h; d.Wx = X->w; d.Cx = X->c;
   d.N = G->n; d.stride = stride; d.T = k * k; d.x_op = AOP_NONE;
   d.generic = (X->c % 4 != 0) || (X->sc != 1);
+  d.x3 = (math & IC_MATH_SPLIT) ? 1 : 0;
   int kk_of_t[IC_MAXT];
   for (int t = 0; t < d.T; ++t) {
     d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
@@ -332,6 +333,7 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
     d.Hx = G->h; d.Wx = G->w; d.Cx = Kp; d.stride = 1; d.T = 1; d.dy[0] = 0; d.dx[0] = 0;
     d.xs_c = 1; d.xs_w = Kp; d.xs_h = (long long)G->w * Kp; d.xs_n = (long long)G->h * G->w * Kp;
     d.generic = 0;
+    d.x3 = 0;
   }
   const size_t part = wg_plan(d);
   const size_t cs = db ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
@@ -463,6 +465,16 @@ int ic_conv_transpose2d_dgrad(const ic_act* dy, const float* w, int k, int strid
   return ic_conv_transpose2d_dgrad_ex(dy, w, k, stride, pad, dx, 0, ws, ws_bytes, stream);
 }
 
+size_t ic_conv2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, int math) {
+  size_t n = 0;
+  int rc = wgrad_impl(dy, x, k, stride, pad, nullptr, dy, (float*)1, nullptr, 0, 0, &n, math);
+  return need_or_zero(rc, n);
+}
+int ic_conv2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw, float* db, int math,
+                       void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(dy, x, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
+}
+
 size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {
   size_t n = 0;
   int rc = wgrad_impl(x, dy, k, stride, pad, nullptr, dy, (float*)1, nullptr, 0, 0, &n);
@@ -471,6 +483,16 @@ size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, in
 int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stride, int pad,
                               float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   return wgrad_impl(x, dy, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+size_t ic_conv_transpose2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, int math) {
+  size_t n = 0;
+  int rc = wgrad_impl(x, dy, k, stride, pad, nullptr, dy, (float*)1, nullptr, 0, 0, &n, math);
+  return need_or_zero(rc, n);
+}
+int ic_conv_transpose2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw, float* db,
+                                 int math, void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(x, dy, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
 }
 
 }  // extern "C"

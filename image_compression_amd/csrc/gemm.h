@@ -85,6 +85,7 @@ struct WgDesc {
   FastDiv fd_hw, fd_w;  // divide a pixel index by Hg*Wg and by Wg (set by wg_run)
   int rowfast;     // Wg and pixels-per-split multiples of the 16-pixel K step (set by wg_run)
   float* partial;  // [nsplit][Tp][Cg][ncols]
+  int x3;          // fp32 by exact three-term bf16 split (wg_x3_kernel); cleared by wg_plan when unsupported
   int dy[IC_MAXT], dx[IC_MAXT];
 };
 

@@ -378,6 +378,243 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
     }
 }
 
+
+// ------------------------------------------------------------------ fp32 by exact bf16 split
+// Weight gradient with fp32 arithmetic on the bf16 MFMA (IC_MATH_SPLIT): both
+// operands are split exactly into three bf16 terms (split3_bf16) and the six
+// cross products are accumulated in fp32 on v_mfma_f32_32x32x16_bf16.  The
+// reduction axis (pixels) is the MFMA K axis, but G and X are channel-
+// contiguous (NHWC), so the 16-pixel K step is staged as [pixel][channel] bf16
+// images and the fragments (8 consecutive pixels of one channel per lane) are
+// read transposed with ds_read_b64_tr_b16.  Image rows are 224 bf16 (448 B):
+// the four rows of one transposed read start 48 dwords apart mod 64, so a
+// 32-lane half covers all 64 banks once.
+//
+// One block per CU (4 waves, 96x96 wave tiles, 144 accumulators each, 512
+// registers per lane available): two LDS buffers, one barrier per K step;
+// each step's global loads are issued a full step ahead (register staging,
+// split + store after the step's MFMAs).
+typedef __bf16 wg_bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool ROWFAST, bool XSQ>
+__global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
+  constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int PITCH = 224;                // bf16 per image row
+  constexpr int PLANE = BK * PITCH;         // one part of one operand
+  constexpr int OPER = 3 * PLANE;           // three parts
+  constexpr int STAGE = 2 * OPER;           // G and X
+  constexpr int C4 = BM / 4;                // float4 per staged row (BM == BN)
+  constexpr int QP = BK * C4 / 256;         // float4 per thread per operand
+  static_assert(BM == BN && BK * C4 % 256 == 0, "staging map");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+
+  const int tiles = d.mtiles * d.ntiles;
+  const int nblk = tiles * d.T * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int per_split = tiles * d.T;
+  const int split = wid / per_split;
+  const int bx = wid - split * per_split;
+  const int t = bx / tiles;
+  const int rem = bx - t * tiles;
+  const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
+  const int g0 = mt * BM, c0 = nt * BN;
+  const uint32_t pb = (uint32_t)split * (uint32_t)d.pps;
+  uint32_t pe = pb + (uint32_t)d.pps;
+  if (pe > (uint32_t)d.P) pe = (uint32_t)d.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dyt = d.dy[t], dxt = d.dx[t];
+
+  int srow[QP], scol[QP];
+#pragma unroll
+  for (int q = 0; q < QP; ++q) {
+    const int f = tid + 256 * q;
+    srow[q] = f / C4;
+    scol[q] = (f - (f / C4) * C4) * 4;
+  }
+
+  // two register sets: a step's global loads are issued two steps before its split + store
+  floatx4v g0r[QP], x0r[QP], g1r[QP], x1r[QP];
+  auto gload = [&](uint32_t p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    if (ROWFAST) {
+      // a 16-pixel step never crosses an output row: image / row / first column are uniform
+      const uint32_t img = fdiv(p0, d.fd_hw);
+      const uint32_t rr = p0 - img * d.fd_hw.d;
+      const uint32_t gy = fdiv(rr, d.fd_w);
+      const uint32_t gx0 = rr - gy * d.fd_w.d;
+      const float* gb = d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w;
+      const int iy = (int)gy * d.stride + dyt, ix0 = (int)gx0 * d.stride + dxt;
+      const bool rowok = (unsigned)iy < (unsigned)d.Hx;
+      const float* xb = d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h;
+#pragma unroll
+      for (int q = 0; q < QP; ++q) {
+        // branch-free: padding and out-of-range columns read a zero page
+        const int gcol = g0 + scol[q], xcol = c0 + scol[q];
+        const int ix = ix0 + srow[q] * d.stride;
+        const float* gs = gcol < d.Cg ? gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
+        const float* xs = (rowok && xcol < d.Cx && (unsigned)ix < (unsigned)d.Wx)
+                              ? xb + (long long)ix * d.xs_w + xcol : wg_zero_page;
+        rg[q] = *(const floatx4v*)gs;
+        floatx4v vx = *(const floatx4v*)xs;
+        if (XSQ) vx = vx * vx;
+        rx[q] = vx;
+      }
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < QP; ++q) {
+      const uint32_t p = p0 + srow[q];
+      floatx4v vg = {0.f, 0.f, 0.f, 0.f}, vx = {0.f, 0.f, 0.f, 0.f};
+      if (p < pe) {
+        const uint32_t img = fdiv(p, d.fd_hw);
+        const uint32_t rr = p - img * d.fd_hw.d;
+        const uint32_t gy = fdiv(rr, d.fd_w);
+        const uint32_t gx = rr - gy * d.fd_w.d;
+        const int gcol = g0 + scol[q], xcol = c0 + scol[q];
+        if (gcol < d.Cg)
+          vg = *(const floatx4v*)(d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx * d.gs_w +
+                                  gcol);
+        const int iy = (int)gy * d.stride + dyt, ix = (int)gx * d.stride + dxt;
+        if (xcol < d.Cx && (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx) {
+          vx = *(const floatx4v*)(d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w +
+                                  xcol);
+          if (XSQ) vx = vx * vx;
+        }
+      }
+      rg[q] = vg;
+      rx[q] = vx;
+    }
+  };
+  // split + store one staged float4 of each operand (q), so the store pass can
+  // be spread between the MFMA groups of the previous step
+  auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
+    __bf16* base = lds + buf * STAGE;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const floatx4v v = op == 0 ? rg[q] : rx[q];
+      wg_bf16x4 vh, vm, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 hh, mm, ll;
+        split3_bf16(v[e], hh, mm, ll);
+        vh[e] = hh; vm[e] = mm; vl[e] = ll;
+      }
+      __bf16* dst = base + op * OPER + srow[q] * PITCH + scol[q];
+      *(wg_bf16x4*)dst = vh;
+      *(wg_bf16x4*)(dst + PLANE) = vm;
+      *(wg_bf16x4*)(dst + 2 * PLANE) = vl;
+    }
+  };
+  auto sstore = [&](int buf, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
+#pragma unroll
+    for (int q = 0; q < QP; ++q) sstore_q(buf, q, rg, rx);
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  const int r = lane & 31, h = lane >> 5;
+  // transposed-read address of this lane inside one plane: row 8h + q, column 16*(r>=16) + 4p
+  const int li = lane & 15;
+  const int tr_off = (8 * h + (li >> 2)) * PITCH + 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // step p0 computes LDS buffer `buf`, stores the set holding step p0 + BK into
+  // buf ^ 1 (interleaved with the MFMAs), then reloads that set with step p0 + 3 BK
+  auto step = [&](int p0, int buf, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    const __bf16* sb = lds + buf * STAGE;
+    wg_bf16x8 a[3][TM], bb[3][TN];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const __bf16* src = sb + q * PLANE + tr_off + wm * WM + i * 32;
+        const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
+        const wg_bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
+        a[q][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const __bf16* src = sb + OPER + q * PLANE + tr_off + wn * WN + j * 32;
+        const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
+        const wg_bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
+        bb[q][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    static_assert(QP == TM, "one staged float4 per MFMA row group");
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], bb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[0][j], acc[i][j], 0, 0, 0);
+      }
+      // the next step's split + store, one slice per MFMA row group, interleaved
+      // with its MFMAs (unconditional: near the end it fills an unread buffer)
+      sstore_q(buf ^ 1, i, rg, rx);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+      }
+    }
+    if (p0 + 3 * BK < (int)pe) gload((uint32_t)(p0 + 3 * BK), rg, rx);  // never past the split (row-fast loads are unmasked)
+    __syncthreads();
+  };
+
+  // steps run in pairs (the two register sets alternate statically); an odd
+  // count is padded with one all-zero step in front
+  const int nsteps = pe > pb ? (int)((pe - pb + BK - 1) / BK) : 0;
+  const int q0 = (int)pb - ((nsteps & 1) ? BK : 0);
+  if (nsteps > 0) {
+    if (nsteps & 1) {
+#pragma unroll
+      for (int q = 0; q < QP; ++q) {
+        g0r[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+        x0r[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      gload((uint32_t)q0, g0r, x0r);
+    }
+    sstore(0, g0r, x0r);
+    if (q0 + BK < (int)pe) gload((uint32_t)(q0 + BK), g1r, x1r);
+    if (q0 + 2 * BK < (int)pe) gload((uint32_t)(q0 + 2 * BK), g0r, x0r);
+  }
+  __syncthreads();
+  for (int p0 = q0; p0 < (int)pe; p0 += 2 * BK) {
+    step(p0, 0, g1r, x1r);
+    step(p0 + BK, 1, g0r, x0r);
+  }
+
+  float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int gr = g0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (gr >= d.Cg) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = c0 + wn * WN + j * 32 + r;
+        if (col < d.ncols) slab[(long long)gr * d.ncols + col] = acc[i][j][reg];
+      }
+    }
+}
+
 struct WgRed {
   const float* partial;
   float* out;    // final [g][c][kk] (G == 1) or level-2 partial [G][g][t][c]
@@ -449,6 +686,20 @@ int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
     hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
   else
     hipLaunchKernelGGL((wg_glds_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int wg_x3_launch(const WgDesc& d, hipStream_t s) {
+  dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
+  const bool sq = d.x_op == AOP_SQUARE;
+  if (d.rowfast) {
+    if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3_kernel<true, false>), grid, dim3(256), 0, s, d);
+  } else {
+    if (sq) hipLaunchKernelGGL((wg_x3_kernel<false, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3_kernel<false, false>), grid, dim3(256), 0, s, d);
+  }
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
@@ -553,6 +804,12 @@ int colsum_blocks(long long rows) {
 constexpr int WG_SPG = 32;  // splits summed per thread in the first reduce level
 
 size_t wg_plan(WgDesc& d) {
+  // split kernel: NHWC, 4-aligned channel rows, 192-wide tiles (wg_x3_kernel)
+  auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (d.x3 && (d.generic || d.Cx < 128 || d.Cg < 128 || d.gs_c != 1 || d.xs_c != 1 || d.Cg % 4 || d.Cx % 4 ||
+               !a16(d.g) || !a16(d.x) || d.gs_w % 4 || d.gs_h % 4 || d.gs_n % 4 || d.xs_w % 4 || d.xs_h % 4 ||
+               d.xs_n % 4))
+    d.x3 = 0;
   if (d.generic) { d.bm = 192; d.bn = 64; d.ncols = d.T * d.Cx; }
   else { d.bm = 192; d.bn = (d.Cx >= 128) ? 192 : 64; d.ncols = d.Cx; }
   d.mtiles = ic_cdiv(d.Cg, d.bm);
@@ -562,7 +819,8 @@ size_t wg_plan(WgDesc& d) {
   // one full wave of blocks: 256 CUs x 2 resident blocks = 512 slots, so a
   // grid of just over 512 equal blocks would run at half speed; never fewer
   // than 64 pixels per split
-  long long ns = tiles >= 512 ? 1 : 512 / tiles;
+  const long long slots = d.x3 ? 256 : 512;  // resident blocks: 1 per CU (split kernel) or 2
+  long long ns = tiles >= slots ? 1 : slots / tiles;
   long long maxs = (d.P + 63) / 64;
   if (ns > maxs) ns = maxs;
   if (ns < 1) ns = 1;
@@ -592,6 +850,10 @@ int wg_run(WgDesc& d, hipStream_t s) {
                        d.gs_n % 4 == 0 && d.xs_w % 4 == 0 && d.xs_h % 4 == 0 && d.xs_n % 4 == 0;
   if (!d.generic && (d.xs_c != 1 || d.Cx % 4 != 0)) return IC_ERR_ARG;
   if (d.generic) return wg_launch_t<192, 64, 96, 32, true>(d, s);
+  if (d.x3) {
+    if (!d.g_vec || d.bn != 192 || d.bm != 192) return IC_ERR_ARG;
+    return wg_x3_launch(d, s);
+  }
   if (glds_ok) {
     if (d.bn == 192) return wg_glds_launch_t<192, 192, 96, 96>(d, s);
     return wg_glds_launch_t<192, 64, 96, 32>(d, s);

@@ -124,10 +124,10 @@ class Conv2dFn(Function):
             dw = torch.empty_like(w)
             db = torch.empty(w.shape[0], device=w.device, dtype=w.dtype) if has_b else None
             ax, ag = _lib.act(x), _lib.act(gy)
-            nb = L.ic_conv2d_wgrad_ws(ax, ag, k, stride, padding)
+            nb = L.ic_conv2d_wgrad_ws_ex(ax, ag, k, stride, padding, math)
             buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
-                                         _lib.ptr(buf), nb, st), "conv2d_wgrad")
+            _lib.check(L.ic_conv2d_wgrad_ex(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db), math,
+                                            _lib.ptr(buf), nb, st), "conv2d_wgrad")
         return dx, dw, db, None, None, None, None
 
 
@@ -180,9 +180,9 @@ class ConvTranspose2dFn(Function):
             dw = torch.empty_like(w)
             db = torch.empty(w.shape[1], device=w.device, dtype=w.dtype) if has_b else None
             ax, ag = _lib.act(x), _lib.act(gy)
-            nb = L.ic_conv_transpose2d_wgrad_ws(ax, ag, k, stride, padding)
+            nb = L.ic_conv_transpose2d_wgrad_ws_ex(ax, ag, k, stride, padding, math)
             buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv_transpose2d_wgrad(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db),
+            _lib.check(L.ic_conv_transpose2d_wgrad_ex(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db), math,
                                                    _lib.ptr(buf), nb, st), "conv_transpose2d_wgrad")
         return dx, dw, db, None, None, None, None, None
 

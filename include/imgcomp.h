@@ -109,6 +109,16 @@ size_t ic_conv_transpose2d_dgrad_ws_ex(const ic_act* dy, int k, int stride, int 
 int ic_conv_transpose2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int pad,
                                  const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
 
+/* weight gradients with a math mode: IC_MATH_SPLIT runs the split kernel on 192-channel-tile NHWC
+ * operands (>= 128 channels each side), the fp32 kernel otherwise; IC_MATH_BF16 is ignored here
+ * (weight gradients stay fp32 in config C3). */
+size_t ic_conv2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, int math);
+int ic_conv2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw, float* db,
+                       int math, void* ws, size_t ws_bytes, void* stream);
+size_t ic_conv_transpose2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, int math);
+int ic_conv_transpose2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw,
+                                 float* db, int math, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- GDN: norm = beta + conv1x1(x^2, gamma); y = x / sqrt(norm) (inverse: x * sqrt(norm)).
  *      gamma [C][C], beta [C] (already re-parameterised); x, y, norm share one layout. */
 size_t ic_gdn_fwd_ws(const ic_act* x);

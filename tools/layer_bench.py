@@ -91,6 +91,9 @@ def main():
             fwd = lambda *q: fwd_ex(*q[:8], a.math, *q[8:])  # noqa: E731
             dgws = lambda *q: dgws_ex(*q, a.math)  # noqa: E731
             dg = lambda *q: dg_ex(*q[:6], a.math, *q[6:])  # noqa: E731
+            wg_ex, wgws_ex = getattr(L, pref + "_wgrad_ex"), getattr(L, pref + "_wgrad_ws_ex")
+            wgws = lambda *q: wgws_ex(*q, a.math)  # noqa: E731
+            wg = lambda *q: wg_ex(*q[:7], a.math, *q[7:])  # noqa: E731
         n1 = fws(ax, k, s, p, ay)
         b1 = ws(n1)
         ms = t_ms(lambda: _lib.check(fwd(ax, _lib.ptr(w), _lib.ptr(b), k, s, p, ay, 0, _lib.ptr(b1), n1, st), "fwd"), a.reps, name + " fwd")
