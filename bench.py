@@ -107,7 +107,7 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     achieved = flop / (ms * 1e-3) / 1e12
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
-        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3<128,192,64,96> (fp32 by 3-term bf16 split)"
+        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,true> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
     else:
         peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",

@@ -12,7 +12,10 @@
 #include "gemm.h"
 
 #ifndef IG_X3_REG
-#define IG_X3_REG 1  // 1: register-staged split kernel (ig_kernel_x3); 0: the LDS-DMA one (ig_kernel_x3d, measured slower)
+#define IG_X3_REG 2  // split kernel: 2 swizzled register-staged (ig_kernel_x3s), 1 padded (ig_kernel_x3), 0 LDS-DMA (ig_kernel_x3d); 2 measured fastest
+#endif
+#ifndef IG_X3_M16
+#define IG_X3_M16 true  // ig_kernel_x3s on v_mfma_f32_16x16x32_bf16 (7-8 % faster than 32x32x16 on the conv fwd layers: DVFS holds a higher clock)
 #endif
 #ifndef IG_X3_NST
 #define IG_X3_NST 3  // LDS stages of the LDS-DMA split kernel
@@ -577,6 +580,271 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
   ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
 }
 
+
+// ------------------------------------------------------------------ split, swizzled, MFMA shape choice
+// ig_kernel_x3 with unpadded 64-B LDS rows (32 bf16 of one K chunk) whose four
+// 16-B chunks are XOR-swizzled by row: chunk c of row r sits at
+// c ^ ig_swz(r), ig_swz(r) = (0, 2, 3, 1)[(r >> 2) & 3], which keeps the
+// ds_read_b128 fragment reads of both MFMA shapes on distinct banks in every
+// 16-lane group (and the 8/16-lane write groups on distinct dword banks):
+// 60 KB of LDS per block instead of 77.  M16 selects v_mfma_f32_16x16x32_bf16
+// (16x16 tiles, K 32 per instruction: lane (r16, g) holds 8 k of chunk g)
+// instead of v_mfma_f32_32x32x16_bf16 (lane (r, h) holds chunk 2s + h of K
+// step s): the same cycles per MAC, but the chip may hold a different clock.
+__device__ __forceinline__ int ig_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+template <int TM, int TN>
+__device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P, floatx4v (&acc)[TM][TN], uint32_t M,
+                                              uint32_t m0, int n0, int wm, int wn, int WM, int WN, int lane,
+                                              int split) {
+  // C/D map of the 16x16 MFMA: col = lane & 15, row = 4 * (lane >> 4) + reg
+  const int c16 = lane & 15, g = lane >> 4;
+  if (d.ksplit > 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 16 + 4 * g + reg;
+        if (m >= M) continue;
+        float* prow = d.partial + ((size_t)split * d.Mtot + P.m_off + m) * d.Cout;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WN + j * 16 + c16;
+          if (n < d.Cout) prow[n] = acc[i][j][reg];
+        }
+      }
+    return;
+  }
+  const uint32_t ysc = (uint32_t)d.ys_c;
+  if (d.epi == EPI_NONE || d.epi == EPI_RELU) {
+    float bj[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + c16;
+      nok[j] = n < d.Cout;
+      bj[j] = (d.bias && nok[j]) ? d.bias[n] : 0.f;
+    }
+    const bool relu = d.epi == EPI_RELU;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const uint32_t m = m0 + wm * WM + i * 16 + 4 * g + reg;
+        if (m >= M) continue;
+        float* yo = d.y + ig_out_offset(d, P, m);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = acc[i][j][reg] + bj[j];
+          if (relu) v = v > 0.f ? v : 0.f;
+          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 16 + c16) * ysc] = v;
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const uint32_t m = m0 + wm * WM + i * 16 + 4 * g + reg;
+      if (m >= M) continue;
+      const uint32_t ob = ig_out_offset(d, P, m);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + c16;
+        if (n < d.Cout) ig_store_out(d, acc[i][j][reg], ob + (uint32_t)n * ysc, n);
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool M16>
+__global__ void __launch_bounds__(256, 2) ig_kernel_x3s(const IgDesc d) {
+  constexpr int LDB = 32;
+  constexpr int WAVES_N = BN / WN;
+  constexpr int APASS = BM / 32, BPASS = BN / 64;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(BN % 64 == 0, "B staged 64 rows per pass");
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * BM * LDB];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * BN * LDB];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = P.T * (d.Cin >> 5);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x;
+  const int lrow = tid >> 3, lc4 = tid & 7;   // A: 8 float4 per 32-channel row
+  const int brow = tid >> 2, bq = tid & 3;    // B: 4 x 16 B per 32-wide bf16 row
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[APASS];
+  int a_iy[APASS], a_ix[APASS];
+#pragma unroll
+  for (int p = 0; p < APASS; ++p) {
+    const uint32_t m = m0 + lrow + 32 * p;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[p] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[p] = (int)gx * d.stride;
+    a_off[p] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[p] * xsh + (uint32_t)a_ix[p] * xsw;
+  }
+  const float* __restrict__ xg = d.x;
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  const size_t wplane = (size_t)d.wplane;
+  // swizzled store offsets (rows lrow + 32p / brow + 64p keep bits 2..3 of the row)
+  const int a_st = lrow * LDB + 8 * ((lc4 >> 1) ^ ig_swz(lrow)) + 4 * (lc4 & 1);
+  const int b_st = brow * LDB + 8 * (bq ^ ig_swz(brow));
+
+  floatx4v ra[APASS];
+  bf16x8 rb[3][BPASS];
+  auto gload = [&](int c) {
+    const int cc = c / P.T, t = c - cc * P.T;
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+      const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;
+      ra[p] = *(const floatx4v*)src;
+    }
+    const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 32 + bq * 8;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int p = 0; p < BPASS; ++p) rb[q][p] = *(const bf16x8*)(wb + q * wplane + (size_t)(64 * p) * d.Cin);
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+      bf16x4 vh, vm, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 h, m, l;
+        split3_bf16(ra[p][e], h, m, l);
+        vh[e] = h; vm[e] = m; vl[e] = l;
+      }
+      __bf16* dst = &As[a_st + 32 * p * LDB];
+      *(bf16x4*)dst = vh;
+      *(bf16x4*)(dst + BM * LDB) = vm;
+      *(bf16x4*)(dst + 2 * BM * LDB) = vl;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[q * BN * LDB + b_st + 64 * p * LDB] = rb[q][p];
+  };
+
+  const int lane = tid & 63, w = tid >> 6;
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+
+  if constexpr (M16) {
+    constexpr int TM = WM / 16, TN = WN / 16;
+    const int r = lane & 15, g = lane >> 4;
+    floatx4v acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    if (cb < ce) {
+      gload(cb);
+      sstore();
+    }
+    __syncthreads();
+    const int ch = 8 * (g ^ ig_swz(r));
+    const __bf16* Ard = &As[(wm * WM + r) * LDB + ch];
+    const __bf16* Brd = &Bs[(wn * WN + r) * LDB + ch];
+    for (int c = cb; c < ce; ++c) {
+      if (c + 1 < ce) gload(c + 1);
+      bf16x8 a[3][TM];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 16) * LDB);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bf16x8 b[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+      if (c + 1 < ce) sstore();
+      __syncthreads();
+    }
+    ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
+  } else {
+    constexpr int TM = WM / 32, TN = WN / 32;
+    const int r = lane & 31, h = lane >> 5;
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    if (cb < ce) {
+      gload(cb);
+      sstore();
+    }
+    __syncthreads();
+    const int sw = ig_swz(r);
+    const __bf16* Ard = &As[(wm * WM + r) * LDB];
+    const __bf16* Brd = &Bs[(wn * WN + r) * LDB];
+    for (int c = cb; c < ce; ++c) {
+      if (c + 1 < ce) gload(c + 1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int ch = 8 * ((2 * s2 + h) ^ sw);
+        bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 32) * LDB + ch);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(Brd + (q * BN + j * 32) * LDB + ch);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+          }
+      }
+      __syncthreads();
+      if (c + 1 < ce) sstore();
+      __syncthreads();
+    }
+    ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
+  }
+}
+
 // ------------------------------------------------------------------ split, LDS-DMA staged
 // Same arithmetic as ig_kernel_x3, staged without a VGPR round trip: each
 // 16-channel K chunk (one tap) arrives by LDS-DMA (global_load_lds_dwordx4)
@@ -802,7 +1070,9 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   } else if (d.x3) {
     if constexpr (BN % 64 == 0) {
       if (sq) return IC_ERR_ARG;
-#if IG_X3_REG
+#if IG_X3_REG == 2
+      hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, IG_X3_M16>), grid, dim3(256), 0, s, d);
+#elif IG_X3_REG
       hipLaunchKernelGGL((ig_kernel_x3<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
 #else
       hipLaunchKernelGGL((ig_kernel_x3d<BM, BN, WM, WN, IG_X3_NST>), grid, dim3(256), 0, s, d);
@@ -859,7 +1129,7 @@ size_t ig_plan(IgDesc& d) {
     mtot += M;
     tiles += (long long)P.mtiles * (d.Npad / d.bn);
     const int nch = d.generic ? (d.Kc >> 5)
-                  : P.T * (d.bf16 ? (d.Cin >> 6) : (d.x3 && !IG_X3_REG) ? (d.Cin >> 4) : (d.Cin >> 5));
+                  : P.T * (d.bf16 ? (d.Cin >> 6) : (d.x3 && IG_X3_REG == 0) ? (d.Cin >> 4) : (d.Cin >> 5));
     nchunks_max = nch > nchunks_max ? nch : nchunks_max;
   }
   d.Mtot = mtot;
