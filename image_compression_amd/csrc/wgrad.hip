@@ -13,6 +13,10 @@
 // per operand fragment (ds_read_b32, conflict-free).
 #include "gemm.h"
 
+#ifndef WG_X3_TWO
+#define WG_X3_TWO 0  // split wgrad: 1 = two blocks per CU (swizzled unpadded rows), 0 = one (padded rows)
+#endif
+
 namespace {
 
 template <int BM, int BN, int WM, int WN, bool GEN>
@@ -397,11 +401,15 @@ __global__ void __launch_bounds__(256, 2) wg_glds_kernel(const WgDesc d) {
 typedef __bf16 wg_bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 
-template <bool ROWFAST, bool XSQ>
-__global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
+// TWO: two blocks per CU — unpadded 192-bf16 rows whose 16-B chunks are
+// XOR-swizzled by 4 on rows with bit 1 set (the four rows of a transposed read
+// then start 0 / 32 / 16 / 48 dwords apart mod 64), 74 KB of LDS per block.
+template <bool ROWFAST, bool XSQ, bool TWO>
+__global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d) {
   constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int PITCH = 224;                // bf16 per image row
+  constexpr int PITCH = TWO ? 192 : 224;    // bf16 per image row
+  constexpr int DEPTH = TWO ? 1 : 2;        // register sets of staged loads in flight
   constexpr int PLANE = BK * PITCH;         // one part of one operand
   constexpr int OPER = 3 * PLANE;           // three parts
   constexpr int STAGE = 2 * OPER;           // G and X
@@ -502,7 +510,7 @@ __global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
         split3_bf16(v[e], hh, mm, ll);
         vh[e] = hh; vm[e] = mm; vl[e] = ll;
       }
-      __bf16* dst = base + op * OPER + srow[q] * PITCH + scol[q];
+      __bf16* dst = base + op * OPER + srow[q] * PITCH + (scol[q] ^ (TWO ? ((srow[q] >> 1) & 1) << 5 : 0));
       *(wg_bf16x4*)dst = vh;
       *(wg_bf16x4*)(dst + PLANE) = vm;
       *(wg_bf16x4*)(dst + 2 * PLANE) = vl;
@@ -517,7 +525,9 @@ __global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
   const int r = lane & 31, h = lane >> 5;
   // transposed-read address of this lane inside one plane: row 8h + q, column 16*(r>=16) + 4p
   const int li = lane & 15;
-  const int tr_off = (8 * h + (li >> 2)) * PITCH + 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  const int tr_row = (8 * h + (li >> 2)) * PITCH;
+  const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  const int tr_sw = TWO ? ((li >> 3) & 1) << 5 : 0;  // rows 8h + (li >> 2) (+4): bit 1 = bit 3 of li
   floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -530,37 +540,31 @@ __global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
   // buf ^ 1 (interleaved with the MFMAs), then reloads that set with step p0 + 3 BK
   auto step = [&](int p0, int buf, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
     const __bf16* sb = lds + buf * STAGE;
-    wg_bf16x8 a[3][TM], bb[3][TN];
+    auto tr8 = [&](const __bf16* src) {
+      const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
+      const wg_bf16x4 hi =
+          __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
+      return (wg_bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    wg_bf16x8 bb[3][TN];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 3; ++q)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const __bf16* src = sb + q * PLANE + tr_off + wm * WM + i * 32;
-        const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
-        const wg_bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
-        a[q][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const __bf16* src = sb + OPER + q * PLANE + tr_off + wn * WN + j * 32;
-        const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
-        const wg_bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
-        bb[q][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-    }
+      for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
     static_assert(QP == TM, "one staged float4 per MFMA row group");
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      wg_bf16x8 a[3];  // one row group's A fragments at a time (register pressure)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE + tr_row + ((wm * WM + i * 32 + tr_col) ^ tr_sw));
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], bb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[2][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
       }
       // the next step's split + store, one slice per MFMA row group, interleaved
       // with its MFMAs (unconditional: near the end it fills an unread buffer)
@@ -572,12 +576,15 @@ __global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
       }
     }
-    if (p0 + 3 * BK < (int)pe) gload((uint32_t)(p0 + 3 * BK), rg, rx);  // never past the split (row-fast loads are unmasked)
+    // refill the set just stored: DEPTH steps ahead (never past the split: row-fast loads are unmasked)
+    if (p0 + (DEPTH + 1) * BK < (int)pe) gload((uint32_t)(p0 + (DEPTH + 1) * BK), rg, rx);
     __syncthreads();
   };
 
-  // steps run in pairs (the two register sets alternate statically); an odd
-  // count is padded with one all-zero step in front
+  // steps run in pairs (with DEPTH 2 the two register sets alternate
+  // statically); an odd count is padded with one all-zero step in front
+  auto& g1s = DEPTH == 2 ? g1r : g0r;
+  auto& x1s = DEPTH == 2 ? x1r : x0r;
   const int nsteps = pe > pb ? (int)((pe - pb + BK - 1) / BK) : 0;
   const int q0 = (int)pb - ((nsteps & 1) ? BK : 0);
   if (nsteps > 0) {
@@ -591,12 +598,12 @@ __global__ void __launch_bounds__(256, 1) wg_x3_kernel(const WgDesc d) {
       gload((uint32_t)q0, g0r, x0r);
     }
     sstore(0, g0r, x0r);
-    if (q0 + BK < (int)pe) gload((uint32_t)(q0 + BK), g1r, x1r);
-    if (q0 + 2 * BK < (int)pe) gload((uint32_t)(q0 + 2 * BK), g0r, x0r);
+    if (q0 + BK < (int)pe) gload((uint32_t)(q0 + BK), g1s, x1s);
+    if (DEPTH == 2 && q0 + 2 * BK < (int)pe) gload((uint32_t)(q0 + 2 * BK), g0r, x0r);
   }
   __syncthreads();
   for (int p0 = q0; p0 < (int)pe; p0 += 2 * BK) {
-    step(p0, 0, g1r, x1r);
+    step(p0, 0, g1s, x1s);
     step(p0 + BK, 1, g0r, x0r);
   }
 
@@ -693,12 +700,13 @@ int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
 int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   const bool sq = d.x_op == AOP_SQUARE;
+  constexpr bool TWO = WG_X3_TWO;
   if (d.rowfast) {
-    if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((wg_x3_kernel<true, false>), grid, dim3(256), 0, s, d);
+    if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true, TWO>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3_kernel<true, false, TWO>), grid, dim3(256), 0, s, d);
   } else {
-    if (sq) hipLaunchKernelGGL((wg_x3_kernel<false, true>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((wg_x3_kernel<false, false>), grid, dim3(256), 0, s, d);
+    if (sq) hipLaunchKernelGGL((wg_x3_kernel<false, true, TWO>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3_kernel<false, false, TWO>), grid, dim3(256), 0, s, d);
   }
   IC_CHECK_LAUNCH();
   return IC_OK;
@@ -819,7 +827,7 @@ size_t wg_plan(WgDesc& d) {
   // one full wave of blocks: 256 CUs x 2 resident blocks = 512 slots, so a
   // grid of just over 512 equal blocks would run at half speed; never fewer
   // than 64 pixels per split
-  const long long slots = d.x3 ? 256 : 512;  // resident blocks: 1 per CU (split kernel) or 2
+  const long long slots = (d.x3 && !WG_X3_TWO) ? 256 : 512;  // resident blocks: 1 or 2 per CU
   long long ns = tiles >= slots ? 1 : slots / tiles;
   long long maxs = (d.P + 63) / 64;
   if (ns > maxs) ns = maxs;
