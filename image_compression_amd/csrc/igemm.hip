@@ -17,6 +17,9 @@
 #ifndef IG_X3_M16
 #define IG_X3_M16 true  // ig_kernel_x3s on v_mfma_f32_16x16x32_bf16 (7-8 % faster than 32x32x16 on the conv fwd layers: DVFS holds a higher clock)
 #endif
+#ifndef IG_X3_BM64
+#define IG_X3_BM64 0  // 1: 64-row tiles (3 blocks per CU) for every split-kernel layer
+#endif
 #ifndef IG_X3_NST
 #define IG_X3_NST 3  // LDS stages of the LDS-DMA split kernel
 #endif
@@ -658,7 +661,7 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
 }
 
 template <int BM, int BN, int WM, int WN, bool M16>
-__global__ void __launch_bounds__(256, 2) ig_kernel_x3s(const IgDesc d) {
+__global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgDesc d) {
   constexpr int LDB = 32;
   constexpr int WAVES_N = BN / WN;
   constexpr int APASS = BM / 32, BPASS = BN / 64;
@@ -1109,7 +1112,7 @@ size_t ig_plan(IgDesc& d) {
   if (d.Cout % 192 == 0) {
     // small maps (hyperprior and <= 32x32 at batch 32): 64-row tiles double the tile
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
-    d.bm = (!d.bf16 && mall < 65536) ? 64 : 128;
+    d.bm = (!d.bf16 && (mall < 65536 || (IG_X3_BM64 && d.x3))) ? 64 : 128;
     d.bn = 192;
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
