@@ -90,7 +90,7 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
 
 int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
-                 size_t* need) {
+                 size_t* need, int math = 0) {
   const long long n = act_numel(x);
   const long long P = (long long)x->n * x->h * x->w;
   // fused path: x, dx, norm, dy all NHWC-dense with x's strides; its workspace
@@ -99,7 +99,8 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
   if (!need && gdn_fused_ok(x->data, dx->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
       wsb >= fused_ws)
-    return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s);
+    return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s,
+                         (math & IC_MATH_SPLIT) ? 1 : 0);
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};
@@ -180,6 +181,12 @@ int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float*
                void* stream) {
   return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes,
                       (hipStream_t)stream, nullptr);
+}
+
+int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                  const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream) {
+  return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,
+                      math);
 }
 
 }  // extern "C"

@@ -204,9 +204,12 @@ __global__ void __launch_bounds__(256, 2)
 // ============================================================== backward
 // phase A of one tile (elementwise, identical swizzled offsets in every image):
 // q = dL/dnorm, and the direct term dy*norm^-1/2 (IGDN: dy*norm^1/2) over dy
-template <int C, int BM>
+// X3: also write q and x^2, split into three bf16 terms, as [pixel][channel]
+// images (sb: q planes then x^2 planes, unpadded C-wide rows whose 16-B chunks
+// are XOR-swizzled by 4 on rows with bit 1 set) for the split dgamma GEMM
+template <int C, int BM, bool X3 = false>
 __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
-                                                uint32_t P, int inverse, int tid) {
+                                                uint32_t P, int inverse, int tid, __bf16* sb = nullptr) {
   constexpr int NCH = BM * C / 4;
   for (int pos = tid; pos < NCH; pos += 512) {
     const int off = pos * 4;
@@ -232,6 +235,26 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
     }
     *(floatx4v*)(qs + off) = qv;
     *(floatx4v*)(gs + off) = dv;
+    if constexpr (X3) {
+      typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+      const int m = pos / (C / 4), lc = (pos - m * (C / 4)) ^ (m & 15);
+      const int col = (4 * lc) ^ (((m >> 1) & 1) << 5);
+      constexpr int PL = BM * C;  // one plane
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        b4 vh, vm, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          __bf16 hh, mm, ll;
+          split3_bf16(op == 0 ? qv[e] : xv[e] * xv[e], hh, mm, ll);
+          vh[e] = hh; vm[e] = mm; vl[e] = ll;
+        }
+        __bf16* dst = sb + op * 3 * PL + m * C + col;
+        *(b4*)dst = vh;
+        *(b4*)(dst + PL) = vm;
+        *(b4*)(dst + 2 * PL) = vl;
+      }
+    }
   }
 }
 
@@ -269,11 +292,19 @@ __device__ unsigned long long gdn_prof[256 * 8 * 16 * 6];
 // (group B) accumulate dgamma (C x C, in VGPRs) and dbeta.  The groups run
 // separate loops with the same barrier sequence per tile (B1 top, B2 after
 // phase A, B3 before the copy-out), so each keeps only its own registers.
-template <int C>
+//
+// X3 (C = 192, IC_MATH_SPLIT): group B's dgamma GEMM runs in split arithmetic
+// (fp32 via three bf16 terms, six v_mfma_f32_32x32x16_bf16 products, fp32
+// accumulation): phase A also writes q and x^2 as split bf16 [pixel][channel]
+// images, read transposed (ds_read_b64_tr_b16, 8 pixels of one channel per
+// lane); waves 4-7 own 96x96 quadrants of dgamma.  Group A's dx GEMM keeps
+// gamma in VGPRs on the fp32 MFMA.
+template <int C, bool X3>
 __global__ void __launch_bounds__(512, 2)
     gdn_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
                          const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
                          float* __restrict__ slab, uint32_t P) {
+  static_assert(!X3 || C == 192, "split dgamma tiles 192 x 192 as 2 x 2 quadrants of 96");
   constexpr int BM = 16;
   constexpr int NTA = 256;       // threads of group A (staging / copy-out)
   constexpr int W4 = C / 4;      // channels per wave slice
@@ -284,6 +315,7 @@ __global__ void __launch_bounds__(512, 2)
   constexpr int NSTORE = BM * C / 4 / NTA;
   // per buffer: x, norm, dy images; plus the q image
   __shared__ __attribute__((aligned(16))) float lds[7 * TILE];
+  __shared__ __attribute__((aligned(16))) __bf16 sbf[X3 ? 6 * TILE : 8];  // split q / x^2 images
   float* const qs = lds + 6 * TILE;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -321,7 +353,7 @@ __global__ void __launch_bounds__(512, 2)
       const uint32_t nxt = tile + gridDim.x;
       float* xs = lds + buf * 3 * TILE;
       float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
-      gdn_bwd_phase_a<C, BM>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid);
+      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
       GDN_MARK(it, 2);
@@ -361,6 +393,79 @@ __global__ void __launch_bounds__(512, 2)
       store_tile<C, BM, NTA>(dx, tile * BM, P, gs, tid);
       buf ^= 1;
     }
+  } else if constexpr (X3) {
+    // ---------------- group B, split: dgamma[n][k] += sum_m q[m][n] x[m][k]^2 on 96x96 quadrants
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    constexpr int PL = TILE;  // bf16 elements per plane
+    const int wq = w - 4, wm2 = wq >> 1, wn2 = wq & 1;
+    const int r = lane & 31, h = lane >> 5;
+    // transposed read of rows 8h + (li >> 2) (+4), columns c0 + 16*(lane>>4 & 1) + 4*(li & 3);
+    // rows with bit 1 set store their chunks XOR 32 bf16
+    const int tr_row = (8 * h + (li >> 2)) * C;
+    const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+    const int tr_sw = ((li >> 3) & 1) << 5;
+    auto tr8 = [&](const __bf16* src) {
+      const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)src);
+      const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * C));
+      return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    floatx16 acc[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    float db = 0.f;
+    const int t = tid - 256;
+    int buf = 0;
+    int it = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // B1
+      const float* xs = lds + buf * 3 * TILE;
+      const uint32_t m0 = tile * BM;
+      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
+      bar_wait_lgkm();  // B2
+      if (t < C) {
+        const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
+        for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
+      }
+      b8 bb[3][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) bb[q][j] = tr8(sbf + 3 * PL + q * PL + tr_row + ((96 * wn2 + 32 * j + tr_col) ^ tr_sw));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        b8 a[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[q] = tr8(sbf + q * PL + tr_row + ((96 * wm2 + 32 * i + tr_col) ^ tr_sw));
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
+        }
+      }
+      bar_wait_lgkm();  // B3
+      buf ^= 1;
+    }
+    float* out = slab + (size_t)blockIdx.x * (C * C + C);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        // C/D map of the 32x32 MFMA: row (A index n) = (reg&3) + 8(reg>>2) + 4h, col (B index k) = lane&31
+        const int n = 96 * wm2 + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) out[(size_t)n * C + 96 * wn2 + 32 * j + r] = acc[i][j][reg];
+      }
+    if (t < C) out[C * C + t] = db;
   } else {
     // ---------------- group B: dgamma[n][k] += sum_m q[m][n] x[m][k]^2, rows n = wbase + 16i + li
     floatx4v dg[NTW][KT];
@@ -378,7 +483,7 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
-      gdn_bwd_phase_a<C, BM>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid);
+      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
       GDN_MARK(it, 2);
@@ -497,13 +602,13 @@ int bwd_grid(long long P) {
   return (int)(ntiles < 256 ? ntiles : 256);
 }
 
-template <int C>
+template <int C, bool X3 = false>
 int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
                          float* dx, float* dgamma, float* dbeta, long long P, float* slab, hipStream_t s) {
   const int grid = bwd_grid(P);
   if (grid < 1) return IC_OK;
-  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx, slab,
-                     (uint32_t)P);
+  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx,
+                     slab, (uint32_t)P);
   IC_CHECK_LAUNCH();
   const int stride = C * C + C;
   hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
@@ -537,8 +642,10 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
 size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * (C * C + C) * sizeof(float); }
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
-                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s) {
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split) {
   float* slab = (float*)ws;
+  if (split && C == 192)
+    return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
   switch (C) {
     case 64: return gdn_bwd_fused_launch<64>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
     case 128: return gdn_bwd_fused_launch<128>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);

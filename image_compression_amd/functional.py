@@ -209,7 +209,7 @@ class GDNFn(Function):
     """modelling/layers/gdn.py:84-86 given re-parameterised gamma (C,C,1,1), beta (C,)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, inverse):
+    def forward(ctx, x, gamma, beta, inverse, math=0):
         _lib.require_device(x, gamma, beta)
         L = _L()
         x = _cl(x)
@@ -223,6 +223,7 @@ class GDNFn(Function):
         _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(b), int(inverse), ay, _lib.ptr(norm), _lib.ptr(buf),
                                 nb, _lib.stream_of(x)), "gdn_fwd")
         ctx.inverse = int(inverse)
+        ctx.math = int(math)
         ctx.save_for_backward(x, norm, g)
         return y
 
@@ -237,13 +238,14 @@ class GDNFn(Function):
         ax, adx = _lib.act(x), _lib.act(dx)
         nb = L.ic_gdn_bwd_ws(ax)
         buf = _ws(nb, x.device)
-        _lib.check(L.ic_gdn_bwd(ax, _lib.ptr(norm), _lib.ptr(gy), _lib.ptr(g), ctx.inverse, adx, _lib.ptr(dg),
-                                _lib.ptr(dbeta), _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_bwd")
-        return dx, dg, dbeta, None
+        _lib.check(L.ic_gdn_bwd_ex(ax, _lib.ptr(norm), _lib.ptr(gy), _lib.ptr(g), ctx.inverse, adx, _lib.ptr(dg),
+                                   _lib.ptr(dbeta), ctx.math, _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_bwd")
+        return dx, dg, dbeta, None, None
 
 
-def gdn(x, gamma, beta, inverse=False):
-    return GDNFn.apply(x, gamma, beta, bool(inverse))
+def gdn(x, gamma, beta, inverse=False, math=0):
+    """`math` 2 (fp32_split): the backward's dgamma GEMM in split arithmetic (C = 192)."""
+    return GDNFn.apply(x, gamma, beta, bool(inverse), int(math))
 
 
 class NonNegFn(Function):

@@ -26,6 +26,8 @@ class NonNegativeParam(nn.Module):
 
 
 class GDN(nn.Module):
+    math = 0   # IC_MATH_*: 2 forms the backward's dgamma in split arithmetic (C = 192; measured slower, off by default)
+
     def __init__(self, in_channels, inverse=False, relu=False,
                  gamma_init=0.1, beta_min=1e-6, offset=2 ** -18):
         super().__init__()
@@ -40,4 +42,4 @@ class GDN(nn.Module):
     def forward(self, x):
         if self.relu:
             x = ReLUFn.apply(x)
-        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse))
+        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse), int(self.math))

@@ -22,16 +22,19 @@ def set_compute_dtype(model, dtype):
     the main transforms (g_a, g_s) only — 97 % of the model's FLOPs; the
     hyperprior transforms (1.3 % of the FLOPs, but they shape the rate term's
     gradients) stay fp32.  Weight gradients, GDN, the entropy models and the
-    3-channel image edges compute in fp32 in every mode."""
+    3-channel image edges compute in fp32 in every mode (GDN's backward can
+    form dgamma in split arithmetic, GDN.math = 2, but measured 4-10 % slower:
+    its fused kernel is not paced by that GEMM)."""
     from ...functional import MATH
     from ..layers.conv import Conv2d, ConvTranspose2d
+    from ..layers.gdn import GDN
     if dtype not in MATH:
         raise ValueError(f"compute dtype {dtype!r}: expected one of {sorted(MATH)}")
     subs = ("analysis_transform", "synthesis_transform")
     if dtype == "fp32_split":
         subs += ("prior_analysis", "prior_synthesis")
     for m in model.modules():
-        if isinstance(m, (Conv2d, ConvTranspose2d)):
+        if isinstance(m, (Conv2d, ConvTranspose2d, GDN)):
             m.math = 0
     for name in subs:
         sub = getattr(model, name, None)

@@ -128,6 +128,10 @@ size_t ic_gdn_bwd_ws(const ic_act* x);
 int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                void* stream);
+/* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three
+ * bf16 terms on the bf16 MFMA); dx and every other case stay on the fp32 MFMA. */
+int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                  const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- elementwise on dense storage of n elements ---- */
 /* NonNegativeParam: v = max(p, bound); out = v*v - ped */

@@ -128,8 +128,9 @@ def main():
         dbe = torch.empty_like(be)
         n2 = L.ic_gdn_bwd_ws(ax)
         b2 = ws(n2)
-        ms = t_ms(lambda: _lib.check(L.ic_gdn_bwd(ax, _lib.ptr(nrm), _lib.ptr(gy), _lib.ptr(g), 0, _lib.act(dx), _lib.ptr(dg),
-                                                  _lib.ptr(dbe), _lib.ptr(b2), n2, st), "gdnb"), a.reps, name + " gdn_bwd")
+        ms = t_ms(lambda: _lib.check(L.ic_gdn_bwd_ex(ax, _lib.ptr(nrm), _lib.ptr(gy), _lib.ptr(g), 0, _lib.act(dx),
+                                                     _lib.ptr(dg), _lib.ptr(dbe), a.math, _lib.ptr(b2), n2, st), "gdnb"),
+                  a.reps, name + " gdn_bwd")
         rows.append((name, "gdn_bwd", ms, 2 * gf))
 
     h = S
