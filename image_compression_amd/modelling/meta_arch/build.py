@@ -13,18 +13,19 @@ def build_model(cfg):
 
 
 def set_compute_dtype(model, dtype):
-    """Arithmetic of the wide convolution forward / input-gradient GEMMs.
+    """Arithmetic of the wide convolutions' GEMMs.
     "fp32": the fp32 MFMA (an exact fp32 fma chain).  "fp32_split": fp32
     arithmetic on the bf16 MFMA — both operands split exactly into three bf16
     terms, six cross products accumulated in fp32, error of an fp32 fma chain
-    (functional.MATH) — on every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16
-    operands with fp32 accumulation (reduced precision, BASELINE config C3) on
-    the main transforms (g_a, g_s) only — 97 % of the model's FLOPs; the
-    hyperprior transforms (1.3 % of the FLOPs, but they shape the rate term's
-    gradients) stay fp32.  Weight gradients, GDN, the entropy models and the
-    3-channel image edges compute in fp32 in every mode (GDN's backward can
-    form dgamma in split arithmetic, GDN.math = 2, but measured 4-10 % slower:
-    its fused kernel is not paced by that GEMM)."""
+    (functional.MATH) — for the forward, input gradient and weight gradient of
+    every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16 operands with fp32
+    accumulation (reduced precision, BASELINE config C3) for the forward and
+    input gradient of the main transforms (g_a, g_s) only — 97 % of the
+    model's FLOPs; the hyperprior transforms (1.3 % of the FLOPs, but they
+    shape the rate term's gradients) and all weight gradients stay fp32.  GDN,
+    the entropy models and the 3-channel image edges compute in fp32 in every
+    mode (GDN's backward can form dgamma in split arithmetic, GDN.math = 2,
+    but measured 4-10 % slower: its fused kernel is not paced by that GEMM)."""
     from ...functional import MATH
     from ..layers.conv import Conv2d, ConvTranspose2d
     from ..layers.gdn import GDN
