@@ -546,11 +546,15 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
           __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
       return (wg_bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
-    wg_bf16x8 bb[3][TN];
+    // B fragments: all three column groups held across the row groups (one
+    // block per CU), or re-read per (row, column) group (TWO: register budget)
+    wg_bf16x8 bb[3][TWO ? 1 : TN];
+    if constexpr (!TWO) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < 3; ++q)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
+        for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
+    }
     static_assert(QP == TM, "one staged float4 per MFMA row group");
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -559,21 +563,28 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
       for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE + tr_row + ((wm * WM + i * 32 + tr_col) ^ tr_sw));
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
+        const int jb = TWO ? 0 : j;
+        if constexpr (TWO) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bb[q][0] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0][jb], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1][jb], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2][jb], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[0][jb], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[1][jb], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][jb], acc[i][j], 0, 0, 0);
       }
       // the next step's split + store, one slice per MFMA row group, interleaved
       // with its MFMAs (unconditional: near the end it fills an unread buffer)
       sstore_q(buf ^ 1, i, rg, rx);
+      if constexpr (!TWO) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // VALU
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+        for (int k = 0; k < 6; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // VALU
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+        }
       }
     }
     // refill the set just stored: DEPTH steps ahead (never past the split: row-fast loads are unmasked)

@@ -22,7 +22,8 @@ def set_compute_dtype(model, dtype):
     accumulation (reduced precision, BASELINE config C3) for the forward and
     input gradient of the main transforms (g_a, g_s) only — 97 % of the
     model's FLOPs; the hyperprior transforms (1.3 % of the FLOPs, but they
-    shape the rate term's gradients) and all weight gradients stay fp32.  GDN,
+    shape the rate term's gradients) and all weight gradients run in
+    "fp32_split" arithmetic there.  GDN,
     the entropy models and the 3-channel image edges compute in fp32 in every
     mode (GDN's backward can form dgamma in split arithmetic, GDN.math = 2,
     but measured 4-10 % slower: its fused kernel is not paced by that GEMM)."""
@@ -31,17 +32,21 @@ def set_compute_dtype(model, dtype):
     from ..layers.gdn import GDN
     if dtype not in MATH:
         raise ValueError(f"compute dtype {dtype!r}: expected one of {sorted(MATH)}")
-    subs = ("analysis_transform", "synthesis_transform")
-    if dtype == "fp32_split":
-        subs += ("prior_analysis", "prior_synthesis")
+    main = ("analysis_transform", "synthesis_transform")
+    hyper = ("prior_analysis", "prior_synthesis")
+    # IC_MATH_* per transform: bf16 (C3) also runs every weight gradient and the
+    # hyperprior in split arithmetic (fp32-accurate, faster than the fp32 MFMA)
+    split = MATH["fp32_split"]
+    flags = {"fp32": (0, 0), "fp32_split": (split, split), "bf16": (MATH["bf16"] | split, split)}[dtype]
     for m in model.modules():
         if isinstance(m, (Conv2d, ConvTranspose2d, GDN)):
             m.math = 0
-    for name in subs:
-        sub = getattr(model, name, None)
-        if sub is None:
-            continue
-        for m in sub.modules():
-            if isinstance(m, (Conv2d, ConvTranspose2d)):
-                m.math = MATH[dtype]
+    for names, flag in ((main, flags[0]), (hyper, flags[1])):
+        for name in names:
+            sub = getattr(model, name, None)
+            if sub is None:
+                continue
+            for m in sub.modules():
+                if isinstance(m, (Conv2d, ConvTranspose2d)):
+                    m.math = flag
     return model
