@@ -78,6 +78,8 @@ SIGNATURES = {
     "ic_gdn_fwd": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_void, c_size, c_void]),
     "ic_gdn_bwd_ws": (c_size, [_ACT]),
     "ic_gdn_bwd": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_size, c_void]),
+    "ic_gdn_fwd_ws_ex": (c_size, [_ACT, c_int]),
+    "ic_gdn_fwd_ex": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_int, c_void, c_size, c_void]),
     "ic_gdn_bwd_ex": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_int, c_void, c_size,
                               c_void]),
     "ic_nonneg_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void]),

@@ -57,10 +57,12 @@ void gemm1x1(IgDesc& d, const ic_act* x, const ic_act* y) {
 }
 
 int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inverse,
-                 const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+                 const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   const long long P = (long long)x->n * x->h * x->w;
+  // split arithmetic: the implicit GEMM (1x1, x^2 squared in the staging, GDN epilogue)
+  const bool split = (math & IC_MATH_SPLIT) && x->c % 32 == 0 && x->sc == 1 && x->c >= 64;
   // the workspace query answers for the general path (the fused one needs none)
-  if (!need && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
+  if (!need && !split && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
       ((uintptr_t)gamma & 15) == 0) {
     return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s);
@@ -72,8 +74,10 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
   d.a_op = AOP_SQUARE;
   d.aux0 = x->data;
   d.aux_out = norm;
+  d.x3 = split ? 1 : 0;
   const size_t part = ig_plan(d);
-  const size_t wpb = (size_t)d.Npad * d.Kc * 4;
+  const size_t wpb = (size_t)d.Npad * d.Kc * (d.x3 ? 6 : 4);
+  d.wplane = (long long)d.Npad * d.Kc;
   const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
   if (need) { *need = tot; return IC_OK; }
   if (x->sn != y->sn || x->sc != y->sc || x->sh != y->sh || x->sw != y->sw) return IC_ERR_ARG;
@@ -83,7 +87,7 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
   d.partial = part ? cv.take(part) : nullptr;
   d.ph[0].wp = wp;
   const int z = 0;
-  int rc = pack_weights(gamma, x->c, x->c, 1, 0, d.generic, 1, &z, &z, d.Npad, d.Kc, wp, s);
+  int rc = pack_weights(gamma, x->c, x->c, 1, 0, d.generic, 1, &z, &z, d.Npad, d.Kc, wp, s, d.x3 ? 2 : 0);
   if (rc) return rc;
   return ig_run(d, s);
 }
@@ -183,6 +187,15 @@ int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float*
                       (hipStream_t)stream, nullptr);
 }
 
+int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
+                  int math, void* ws, size_t ws_bytes, void* stream) {
+  return gdn_fwd_impl(x, gamma, beta, inverse, y, norm, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
+}
+size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math) {
+  size_t n = 0;
+  gdn_fwd_impl(x, nullptr, nullptr, 0, x, nullptr, nullptr, 0, 0, &n, math);
+  return n;
+}
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream) {
   return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,

@@ -730,6 +730,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
 #pragma unroll
       for (int p = 0; p < BPASS; ++p) rb[q][p] = *(const bf16x8*)(wb + q * wplane + (size_t)(64 * p) * d.Cin);
   };
+  const bool sq = d.a_op == AOP_SQUARE;  // GDN's x^2 (uniform)
   auto sstore = [&]() {
 #pragma unroll
     for (int p = 0; p < APASS; ++p) {
@@ -737,7 +738,7 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         __bf16 h, m, l;
-        split3_bf16(ra[p][e], h, m, l);
+        split3_bf16(sq ? ra[p][e] * ra[p][e] : ra[p][e], h, m, l);
         vh[e] = h; vm[e] = m; vl[e] = l;
       }
       __bf16* dst = &As[a_st + 32 * p * LDB];
@@ -1072,12 +1073,13 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
     hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
   } else if (d.x3) {
     if constexpr (BN % 64 == 0) {
-      if (sq) return IC_ERR_ARG;
 #if IG_X3_REG == 2
       hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, IG_X3_M16>), grid, dim3(256), 0, s, d);
 #elif IG_X3_REG
+      if (sq) return IC_ERR_ARG;
       hipLaunchKernelGGL((ig_kernel_x3<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
 #else
+      if (sq) return IC_ERR_ARG;
       hipLaunchKernelGGL((ig_kernel_x3d<BM, BN, WM, WN, IG_X3_NST>), grid, dim3(256), 0, s, d);
 #endif
     } else {
@@ -1159,7 +1161,7 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.Mtot == 0) return IC_OK;
   if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
   if (d.bf16 && (d.generic || d.Cin % 64 != 0)) return IC_ERR_ARG;
-  if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op != AOP_NONE || d.bn % 64 != 0)) return IC_ERR_ARG;
+  if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
   if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);

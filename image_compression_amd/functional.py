@@ -209,7 +209,7 @@ class GDNFn(Function):
     """modelling/layers/gdn.py:84-86 given re-parameterised gamma (C,C,1,1), beta (C,)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, inverse, math=0):
+    def forward(ctx, x, gamma, beta, inverse, math=0, math_fwd=0):
         _lib.require_device(x, gamma, beta)
         L = _L()
         x = _cl(x)
@@ -218,10 +218,10 @@ class GDNFn(Function):
         y = torch.empty_like(x)
         norm = torch.empty_like(x)
         ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_gdn_fwd_ws(ax)
+        nb = L.ic_gdn_fwd_ws_ex(ax, int(math_fwd))
         buf = _ws(nb, x.device)
-        _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(b), int(inverse), ay, _lib.ptr(norm), _lib.ptr(buf),
-                                nb, _lib.stream_of(x)), "gdn_fwd")
+        _lib.check(L.ic_gdn_fwd_ex(ax, _lib.ptr(g), _lib.ptr(b), int(inverse), ay, _lib.ptr(norm), int(math_fwd),
+                                   _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_fwd")
         ctx.inverse = int(inverse)
         ctx.math = int(math)
         ctx.save_for_backward(x, norm, g)
@@ -240,12 +240,13 @@ class GDNFn(Function):
         buf = _ws(nb, x.device)
         _lib.check(L.ic_gdn_bwd_ex(ax, _lib.ptr(norm), _lib.ptr(gy), _lib.ptr(g), ctx.inverse, adx, _lib.ptr(dg),
                                    _lib.ptr(dbeta), ctx.math, _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_bwd")
-        return dx, dg, dbeta, None, None
+        return dx, dg, dbeta, None, None, None
 
 
-def gdn(x, gamma, beta, inverse=False, math=0):
-    """`math` 2 (fp32_split): the backward's dgamma GEMM in split arithmetic (C = 192)."""
-    return GDNFn.apply(x, gamma, beta, bool(inverse), int(math))
+def gdn(x, gamma, beta, inverse=False, math=0, math_fwd=0):
+    """`math` 2: the backward's dgamma GEMM in split arithmetic (C = 192); `math_fwd` 2: the
+    forward on the split implicit GEMM instead of the fused fp32 kernel."""
+    return GDNFn.apply(x, gamma, beta, bool(inverse), int(math), int(math_fwd))
 
 
 class NonNegFn(Function):

@@ -26,7 +26,8 @@ class NonNegativeParam(nn.Module):
 
 
 class GDN(nn.Module):
-    math = 0   # IC_MATH_*: 2 forms the backward's dgamma in split arithmetic (C = 192; measured slower, off by default)
+    math = 0       # IC_MATH_*: 2 forms the backward's dgamma in split arithmetic (C = 192; measured slower, off by default)
+    math_fwd = 0   # IC_MATH_*: 2 runs the forward on the split implicit GEMM (set_compute_dtype)
 
     def __init__(self, in_channels, inverse=False, relu=False,
                  gamma_init=0.1, beta_min=1e-6, offset=2 ** -18):
@@ -42,4 +43,4 @@ class GDN(nn.Module):
     def forward(self, x):
         if self.relu:
             x = ReLUFn.apply(x)
-        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse), int(self.math))
+        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse), int(self.math), int(self.math_fwd))

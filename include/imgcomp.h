@@ -128,6 +128,11 @@ size_t ic_gdn_bwd_ws(const ic_act* x);
 int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                void* stream);
+/* math = IC_MATH_SPLIT (C % 32 == 0, C >= 64, channel-contiguous): the forward runs on the split
+ * implicit GEMM (x^2 squared in its staging, the divide in its epilogue) instead of the fused fp32 kernel. */
+size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math);
+int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
+                  int math, void* ws, size_t ws_bytes, void* stream);
 /* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three
  * bf16 terms on the bf16 MFMA); dx and every other case stay on the fp32 MFMA. */
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,

@@ -51,7 +51,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="run only ops whose 'layer op' contains this text")
-    ap.add_argument("--math", type=int, default=0, help="IC_MATH_* of the conv fwd / dgrad (0 fp32, 2 fp32 split)")
+    ap.add_argument("--math", type=int, default=0, help="IC_MATH_* of the conv fwd / dgrad / wgrad (0 fp32, 2 fp32 split)")
+    ap.add_argument("--gdn-math", type=int, default=0, help="IC_MATH_* of the GDN forward")
     a = ap.parse_args()
     global ONLY
     ONLY = a.only
@@ -119,9 +120,10 @@ def main():
         be = torch.ones(c, device="cuda")
         ax, ay = _lib.act(x), _lib.act(y)
         gf = 2.0 * N * h * h * c * c / 1e9
-        n1 = L.ic_gdn_fwd_ws(ax)
+        n1 = L.ic_gdn_fwd_ws_ex(ax, a.gdn_math)
         b1 = ws(n1)
-        ms = t_ms(lambda: _lib.check(L.ic_gdn_fwd(ax, _lib.ptr(g), _lib.ptr(be), 0, ay, _lib.ptr(nrm), _lib.ptr(b1), n1, st), "gdn"), a.reps, name + " gdn_fwd")
+        ms = t_ms(lambda: _lib.check(L.ic_gdn_fwd_ex(ax, _lib.ptr(g), _lib.ptr(be), 0, ay, _lib.ptr(nrm), a.gdn_math,
+                                                     _lib.ptr(b1), n1, st), "gdn"), a.reps, name + " gdn_fwd")
         rows.append((name, "gdn_fwd", ms, gf))
         dx = torch.empty_like(x)
         dg = torch.empty_like(g)
