@@ -424,10 +424,13 @@ __global__ void __launch_bounds__(512, 2)
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
+      GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
       gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
+      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
+      GDN_MARK(it, 2);
       if (t < C) {
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
@@ -452,7 +455,10 @@ __global__ void __launch_bounds__(512, 2)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
         }
       }
+      GDN_MARK(it, 3);
+      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
+      GDN_MARK(it, 5);
       buf ^= 1;
     }
     float* out = slab + (size_t)blockIdx.x * (C * C + C);

@@ -5,7 +5,8 @@
 #include <cstdio>
 #include <vector>
 
-int main() {
+template <bool X3>
+void run() {
   const int C = 192;
   const long long P = 32LL * 128 * 128;
   std::vector<float> hx(P * C), hn(P * C), hg(C * C);
@@ -25,13 +26,13 @@ int main() {
   float best = 1e9;
   for (int r = 0; r < 10; ++r) {
     hipEventRecord(e0);
-    hipLaunchKernelGGL((gdn_bwd_fused_kernel<192>), dim3(256), dim3(512), 0, 0, x, n, dy, g, 0, dx, slab, (uint32_t)P);
+    hipLaunchKernelGGL((gdn_bwd_fused_kernel<192, X3>), dim3(256), dim3(512), 0, 0, x, n, dy, g, 0, dx, slab, (uint32_t)P);
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1); if (ms < best) best = ms;
   }
   std::vector<unsigned long long> pr(256 * 8 * 16 * 6);
   hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(gdn_prof), pr.size() * 8);
-  printf("kernel %.3f ms  (tiles/block %lld)\n", best, (P / 16 + 255) / 256);
+  printf("%s: kernel %.3f ms  (tiles/block %lld)\n", X3 ? "split dgamma" : "fp32", best, (P / 16 + 255) / 256);
   const char* names[6] = {"B1", "phaseA", "B2", "gemm", "epi", "B3"};
   for (int w : {0, 4}) {
     double d[6] = {0}, per = 0; int cnt = 0;
@@ -47,5 +48,11 @@ int main() {
     for (int e = 1; e < 6; ++e) printf(" %s->%s %.0f", names[e - 1], names[e], d[e] / cnt);
     printf(" | B3->B1 %.0f\n", d[0] / cnt);
   }
+  hipFree(x); hipFree(n); hipFree(dy); hipFree(dx); hipFree(g); hipFree(slab);
+}
+
+int main() {
+  run<false>();
+  run<true>();
   return 0;
 }
