@@ -3,8 +3,9 @@ each fp32 operand is split exactly into three bf16 terms and the six cross
 products that carry a product to 2^-24 of its size run on the bf16 MFMA with
 fp32 accumulation.  The claim is fp32 accuracy, so the bar is the fp32 one
 (allclose rtol 1e-4, atol 1e-4*max|ref| against the fp64 oracle)
-and, tighter, a normwise error within a small factor of the native fp32
-kernel's own error on the same inputs.  A bitwise difference from the native
+and, tighter, a normwise error within 1.5x of the native fp32 kernel's own
+error on the same inputs (measured 0.7-1.3x: the split is as accurate as the
+fp32 MFMA).  A bitwise difference from the native
 kernel proves the split kernel is the one that ran."""
 import pytest
 import torch
@@ -42,7 +43,9 @@ def _check(split, native, ref, name, ran=True):
     assert_close(split, ref, 1e-4, name)
     es, en = rel_err(split, ref), rel_err(native, ref)
     print(f"{name}: split {es:.2e} native fp32 {en:.2e}")
-    assert es <= 4.0 * en + 1e-7, (name, es, en)     # fp32-class, not bf16-class (~1e-3)
+    # fp32-class, not bf16-class (~1e-3): measured 0.7-1.3x the native fp32 MFMA's own error
+    # (profiles/r01l_split_vs_fp32_errors.log)
+    assert es <= 1.5 * en + 1e-8, (name, es, en)
     if ran:
         assert not torch.equal(split, native), name   # the split kernel ran
 
