@@ -59,13 +59,14 @@ void gemm1x1(IgDesc& d, const ic_act* x, const ic_act* y) {
 int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inverse,
                  const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   const long long P = (long long)x->n * x->h * x->w;
-  // split arithmetic: the implicit GEMM (1x1, x^2 squared in the staging, GDN epilogue)
+  // split arithmetic: the fused split kernel (C = 192), else the implicit GEMM
+  // (1x1, x^2 squared in the staging, GDN epilogue)
   const bool split = (math & IC_MATH_SPLIT) && x->c % 32 == 0 && x->sc == 1 && x->c >= 64;
   // the workspace query answers for the general path (the fused one needs none)
-  if (!need && !split && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
+  if (!need && (!split || x->c == 192) && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
       ((uintptr_t)gamma & 15) == 0) {
-    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s);
+    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s, split ? 1 : 0);
   }
   IgDesc d = {};
   gemm1x1(d, x, y);

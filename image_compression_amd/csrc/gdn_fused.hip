@@ -201,6 +201,124 @@ __global__ void __launch_bounds__(256, 2)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ============================================================== forward, split
+// norm = beta + Gamma x^2 in split arithmetic (fp32 via three bf16 terms, six
+// v_mfma_f32_16x16x32_bf16 products, fp32 accumulation), C = 192.  12 waves
+// (768 threads), one block per CU: wave w owns output channels [16w, 16w+16)
+// and keeps its slice of Gamma, split into three bf16 terms, as B fragments in
+// 72 VGPRs for the whole launch.  Per 32-pixel tile: LDS-DMA of x (two
+// buffers, as the fp32 kernel), one cooperative pass squares x and writes x^2
+// as three bf16 planes (384-B rows, 16-B chunks XOR (row >> 1) & 7: conflict-
+// free 16x16x32 fragment reads), the MFMAs, the epilogue (y over x in place,
+// norm into a staging image), one coalesced copy-out.
+template <int C>
+__global__ void __launch_bounds__(768, 1)
+    gdn_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                      const float* __restrict__ beta, int inverse, float* __restrict__ y,
+                      float* __restrict__ norm, uint32_t P) {
+  static_assert(C == 192, "12 waves x 16 channels");
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  constexpr int BM = 32, NT = 768;
+  constexpr int TILE = BM * C;
+  constexpr int KU = C / 32;                       // 32-wide K chunks
+  constexpr int NSTORE = 2 * (BM * C / 4 / NT);    // vector-memory ops of one copy-out
+  constexpr int QS = BM * C / 4 / NT;              // float4 per thread in the split pass
+  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];  // 2 x-buffers + norm staging
+  __shared__ __attribute__((aligned(16))) __bf16 sq[3 * TILE];   // x^2, three bf16 planes
+  float* const nst = lds + 2 * TILE;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int n = 16 * w + li;  // this lane's output channel (B column / C/D column)
+  const uint32_t ntiles = (P + BM - 1) / BM;
+
+  // Gamma^T fragments: lane (n = li, g) holds k = 32u + 8g .. +7 of row n of Gamma
+  b8 bg[3][KU];
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    const floatx4v g0 = *(const floatx4v*)(gamma + (size_t)n * C + 32 * u + 8 * lg);
+    const floatx4v g1 = *(const floatx4v*)(gamma + (size_t)n * C + 32 * u + 8 * lg + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 hh, mm, ll;
+      split3_bf16(e < 4 ? g0[e] : g1[e - 4], hh, mm, ll);
+      bg[0][u][e] = hh; bg[1][u][e] = mm; bg[2][u][e] = ll;
+    }
+  }
+  const float bet = beta[n];
+  const int fsw = (li >> 1) & 7;  // fragment rows 16mt + li share bits 1..3 of li
+
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) stage_tile<C, BM, NT>(x, tile * BM, P, lds, tid, lane);
+  int buf = 0;
+  bool first = true;
+  for (; tile < ntiles; tile += gridDim.x) {
+    if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+    __builtin_amdgcn_s_barrier();  // B1: tile `buf` landed
+    first = false;
+    const uint32_t nxt = tile + gridDim.x;
+    float* xs = lds + buf * TILE;
+    if (nxt < ntiles) stage_tile<C, BM, NT>(x, nxt * BM, P, lds + (buf ^ 1) * TILE, tid, lane);
+    // x^2 split pass: float4 `pos` of the swizzled fp32 image -> 3 bf16 quads
+#pragma unroll
+    for (int q = 0; q < QS; ++q) {
+      const int pos = tid + NT * q;
+      const int m = pos / (C / 4), lc = (pos - m * (C / 4)) ^ (m & 15);
+      const floatx4v v = *(const floatx4v*)(xs + pos * 4);
+      b4 vh, vm, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 hh, mm, ll;
+        split3_bf16(v[e] * v[e], hh, mm, ll);
+        vh[e] = hh; vm[e] = mm; vl[e] = ll;
+      }
+      const int off = m * C + 8 * ((lc >> 1) ^ ((m >> 1) & 7)) + 4 * (lc & 1);
+      *(b4*)(sq + off) = vh;
+      *(b4*)(sq + TILE + off) = vm;
+      *(b4*)(sq + 2 * TILE + off) = vl;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // B2: x^2 planes complete
+    floatx4v acc[BM / 16];
+#pragma unroll
+    for (int mt = 0; mt < BM / 16; ++mt) {
+      acc[mt] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      const __bf16* ar = sq + (16 * mt + li) * C;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int ch = 8 * ((4 * u + lg) ^ fsw);
+        const b8 a0 = *(const b8*)(ar + ch), a1 = *(const b8*)(ar + TILE + ch), a2 = *(const b8*)(ar + 2 * TILE + ch);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bg[0][u], acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[1][u], acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[2][u], acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[0][u], acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[1][u], acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[0][u], acc[mt], 0, 0, 0);
+      }
+    }
+    // epilogue (C/D map: col n = li, row m = 16mt + 4g + r); y over x in place
+#pragma unroll
+    for (int mt = 0; mt < BM / 16; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int off = swz<C>(16 * mt + 4 * lg + r, n);
+        const float nv = acc[mt][r] + bet;
+        const float xv = xs[off];
+        xs[off] = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
+        nst[off] = nv;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // B3
+    store_tile<C, BM, NT>(y, tile * BM, P, xs, tid);
+    store_tile<C, BM, NT>(norm, tile * BM, P, nst, tid);
+    buf ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ============================================================== backward
 // phase A of one tile (elementwise, identical swizzled offsets in every image):
 // q = dL/dnorm, and the direct term dy*norm^-1/2 (IGDN: dy*norm^1/2) over dy
@@ -636,7 +754,16 @@ bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long
 }
 
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
-                  long long P, hipStream_t s) {
+                  long long P, hipStream_t s, int split) {
+  if (split && C == 192) {
+    const long long ntiles = (P + 31) / 32;
+    const long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
+    if (grid < 1) return IC_OK;
+    hipLaunchKernelGGL((gdn_fwd_x3_kernel<192>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse, y,
+                       norm, (uint32_t)P);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   switch (C) {
     case 64: return gdn_fwd_fused_launch<64>(x, gamma, beta, inverse, y, norm, P, s);
     case 128: return gdn_fwd_fused_launch<128>(x, gamma, beta, inverse, y, norm, P, s);

@@ -121,7 +121,7 @@ int col2im_run(const float* ycol, int ncol, int N, int Hi, int Wi, const float* 
 bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long long sc, long long sw, long long sh,
                   long long sn, int H, int W, long long P);
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
-                  long long P, hipStream_t s);
+                  long long P, hipStream_t s, int split = 0);  // split: C = 192 in split arithmetic
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0);

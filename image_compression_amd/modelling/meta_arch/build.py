@@ -25,11 +25,10 @@ def set_compute_dtype(model, dtype):
     shape the rate term's gradients) and all weight gradients run in
     "fp32_split" arithmetic there.  GDN,
     the entropy models and the 3-channel image edges compute in fp32 in every
-    mode, except that "fp32_split" and "bf16" form GDN's backward dgamma in
-    split arithmetic (GDN.math = 2: 4 % faster fused backward, A/B in one
-    process, tools/gdn_ab.py).  GDN's forward on the split implicit GEMM
-    (GDN.math_fwd = 2) is correct but 1.7x slower than the fused fp32
-    kernel, so it stays off."""
+    mode, except that "fp32_split" and "bf16" run GDN (C = 192) in split
+    arithmetic too: the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at
+    128^2) and the fused backward's dgamma GEMM (GDN.math = 2: 4 % faster);
+    A/B in one process, tools/gdn_ab.py."""
     from ...functional import MATH
     from ..layers.conv import Conv2d, ConvTranspose2d
     from ..layers.gdn import GDN
@@ -45,7 +44,8 @@ def set_compute_dtype(model, dtype):
         if isinstance(m, (Conv2d, ConvTranspose2d, GDN)):
             m.math = 0
         if isinstance(m, GDN) and dtype != "fp32":
-            m.math = split   # the fused backward's dgamma GEMM in split arithmetic
+            m.math = split      # the fused backward's dgamma GEMM in split arithmetic
+            m.math_fwd = split  # the fused forward (C = 192) in split arithmetic
     for names, flag in ((main, flags[0]), (hyper, flags[1])):
         for name in names:
             sub = getattr(model, name, None)

@@ -128,8 +128,9 @@ size_t ic_gdn_bwd_ws(const ic_act* x);
 int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                void* stream);
-/* math = IC_MATH_SPLIT (C % 32 == 0, C >= 64, channel-contiguous): the forward runs on the split
- * implicit GEMM (x^2 squared in its staging, the divide in its epilogue) instead of the fused fp32 kernel. */
+/* math = IC_MATH_SPLIT (C % 32 == 0, C >= 64, channel-contiguous): the forward runs in split arithmetic —
+ * the fused kernel for NHWC-dense C = 192, otherwise the split implicit GEMM (x^2 squared in its staging,
+ * the divide in its epilogue). */
 size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math);
 int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
                   int math, void* ws, size_t ws_bytes, void* stream);

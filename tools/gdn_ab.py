@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the fused GDN backward, fp32 dgamma (math 0) vs split dgamma (math 2),
-alternating in one process on the 128x128 and 64x64 C2 shapes.  GPU only."""
+"""A/B of the fused GDN kernels in one process, alternating, on the 128x128
+and 64x64 C2 shapes: backward with fp32 dgamma (math 0) vs split dgamma
+(math 2); forward fp32 (math 0) vs split (math 2).  GPU only."""
 import os
 import sys
 
@@ -40,8 +41,27 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[m].append(e0.elapsed_time(e1) / 10)
-        print(f"{h}x{h}: fp32 dgamma {min(res[0]):.3f} ms (median {sorted(res[0])[3]:.3f}), "
+        print(f"{h}x{h}: bwd fp32 dgamma {min(res[0]):.3f} ms (median {sorted(res[0])[3]:.3f}), "
               f"split dgamma {min(res[2]):.3f} ms (median {sorted(res[2])[3]:.3f})")
+        y = torch.empty_like(x)
+        ay = _lib.act(y)
+        be = torch.ones(C, device="cuda")
+        res = {0: [], 2: []}
+        for rep in range(6):
+            for m in (0, 2):
+                nb = L.ic_gdn_fwd_ws_ex(ax, m)
+                wsf = _lib.workspace(max(nb, 256), "cuda")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for _ in range(2):
+                    L.ic_gdn_fwd_ex(ax, _lib.ptr(gam), _lib.ptr(be), 0, ay, _lib.ptr(nrm), m, _lib.ptr(wsf), nb, st)
+                e0.record()
+                for _ in range(10):
+                    L.ic_gdn_fwd_ex(ax, _lib.ptr(gam), _lib.ptr(be), 0, ay, _lib.ptr(nrm), m, _lib.ptr(wsf), nb, st)
+                e1.record()
+                torch.cuda.synchronize()
+                res[m].append(e0.elapsed_time(e1) / 10)
+        print(f"{h}x{h}: fwd fp32 {min(res[0]):.3f} ms (median {sorted(res[0])[3]:.3f}), "
+              f"split {min(res[2]):.3f} ms (median {sorted(res[2])[3]:.3f})")
 
 
 if __name__ == "__main__":
