@@ -134,8 +134,11 @@ int ic_gdn_bwd(const ic_act* x, const float* norm, const float* dy, const float*
 size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math);
 int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
                   int math, void* ws, size_t ws_bytes, void* stream);
-/* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three
- * bf16 terms on the bf16 MFMA); dx and every other case stay on the fp32 MFMA. */
+/* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three bf16
+ * terms on the bf16 MFMA), dx on the fp32 MFMA; IC_MATH_SPLIT | IC_MATH_GDN_BWD_FULL_SPLIT runs dx in split
+ * arithmetic too (12-wave kernel; measured no faster: register-bound at 16-pixel tiles).  Other shapes stay
+ * on the fp32 MFMA. */
+#define IC_MATH_GDN_BWD_FULL_SPLIT 8
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
 

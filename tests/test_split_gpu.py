@@ -150,7 +150,7 @@ def test_gdn_split_dgamma(n, h, w, inverse):
     gy = _r(*yr.shape, seed=13)
     yr.backward(gy.double())
     out = {}
-    for math in (2, 0):
+    for math in (2, 0, 2 | 8):   # split dgamma, fp32, split dx + dgamma (IC_MATH_GDN_BWD_FULL_SPLIT)
         md = m.to(DEV)
         md.math = math
         md.zero_grad()
@@ -160,6 +160,9 @@ def test_gdn_split_dgamma(n, h, w, inverse):
     _check(out[2][1], out[0][1], gp.grad, "dgamma")
     assert_close(out[2][0], xr.grad, 1e-4, "dx")
     assert_close(out[2][2], bp.grad, 1e-4, "dbeta")
+    _check(out[10][1], out[0][1], gp.grad, "dgamma (full split)")
+    _check(out[10][0], out[0][0], xr.grad, "dx (full split)")
+    assert_close(out[10][2], bp.grad, 1e-4, "dbeta (full split)")
 
 
 @pytest.mark.parametrize("n,c,h,w,inverse", [(2, 192, 16, 16, False), (3, 192, 7, 5, True), (2, 64, 9, 9, False)])
