@@ -13,6 +13,9 @@
 // per operand fragment (ds_read_b32, conflict-free).
 #include "gemm.h"
 
+#ifndef WG_X3_PAIR
+#define WG_X3_PAIR 0  // 1: one 8-wave block per CU over two taps (wg_x3p_kernel; measured 19 % slower)
+#endif
 #ifndef WG_X3_TWO
 #define WG_X3_TWO 0  // split wgrad: 1 = two blocks per CU (swizzled unpadded rows), 0 = one (padded rows)
 #endif
@@ -633,6 +636,196 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
     }
 }
 
+
+// Tap-pair variant: one block of 8 waves per CU computes the weight gradient
+// of TWO taps over the same pixel range — waves 0-3 tap 2tp, waves 4-7 tap
+// 2tp+1, each as the 4-wave kernel above (96x96 wave tiles, 144 AGPR-free
+// accumulators).  The G operand (the same for every tap) is staged once per
+// step for both; two waves per SIMD hide each other's barrier and read
+// latency.  LDS per buffer: G (3 planes) + X of both taps (6 planes), 448-B
+// rows; two buffers (129 KB).
+template <bool ROWFAST, bool XSQ>
+__global__ void __launch_bounds__(512) wg_x3p_kernel(const WgDesc d) {
+  constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int PITCH = 224;
+  constexpr int PLANE = BK * PITCH;
+  constexpr int OPER = 3 * PLANE;
+  constexpr int STAGE = 3 * OPER;           // G, X(tap 0), X(tap 1)
+  constexpr int C4 = BM / 4;                // float4 per staged row
+  constexpr int NSLOT = 3 * BK * C4;        // float4 slots per step (G + 2 X)
+  constexpr int QP = (NSLOT + 511) / 512;   // 5
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+
+  const int tiles = d.mtiles * d.ntiles;
+  const int TP = (d.T + 1) >> 1;            // tap pairs
+  const int nblk = tiles * TP * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int per_split = tiles * TP;
+  const int split = wid / per_split;
+  const int bx = wid - split * per_split;
+  const int tp = bx / tiles;
+  const int rem = bx - tp * tiles;
+  const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
+  const int g0 = mt * BM, c0 = nt * BN;
+  const uint32_t pb = (uint32_t)split * (uint32_t)d.pps;
+  uint32_t pe = pb + (uint32_t)d.pps;
+  if (pe > (uint32_t)d.P) pe = (uint32_t)d.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int t0 = 2 * tp, t1 = 2 * tp + 1;
+  const bool has1 = t1 < d.T;
+  const int dy0 = d.dy[t0], dx0 = d.dx[t0];
+  const int dy1 = has1 ? d.dy[t1] : 0, dx1 = has1 ? d.dx[t1] : 0;
+
+  // staging slots: s < BK*C4 -> G; then X of tap 0, X of tap 1
+  int sop[QP], srow[QP], scol[QP];
+  bool sok[QP];
+#pragma unroll
+  for (int q = 0; q < QP; ++q) {
+    const int f = tid + 512 * q;
+    sok[q] = f < NSLOT && (f < 2 * BK * C4 || has1);
+    const int op = f / (BK * C4), g = f - op * (BK * C4);
+    sop[q] = op;
+    srow[q] = g / C4;
+    scol[q] = (g - (g / C4) * C4) * 4;
+  }
+  floatx4v rs[QP];
+  auto gload = [&](uint32_t p0) {
+    uint32_t img = 0, gy = 0, gx0 = 0;
+    if (ROWFAST) {
+      img = fdiv(p0, d.fd_hw);
+      const uint32_t rr = p0 - img * d.fd_hw.d;
+      gy = fdiv(rr, d.fd_w);
+      gx0 = rr - gy * d.fd_w.d;
+    }
+#pragma unroll
+    for (int q = 0; q < QP; ++q) {
+      const float* src = wg_zero_page;
+      uint32_t im = img, yy = gy, xx = gx0 + srow[q];
+      bool pin = true;
+      if (!ROWFAST) {
+        const uint32_t p = p0 + srow[q];
+        pin = p < pe;
+        const uint32_t pp = pin ? p : 0u;
+        im = fdiv(pp, d.fd_hw);
+        const uint32_t rr = pp - im * d.fd_hw.d;
+        yy = fdiv(rr, d.fd_w);
+        xx = rr - yy * d.fd_w.d;
+      }
+      if (sok[q] && pin) {
+        if (sop[q] == 0) {
+          const int gcol = g0 + scol[q];
+          if (gcol < d.Cg) src = d.g + (long long)im * d.gs_n + (long long)yy * d.gs_h + (long long)xx * d.gs_w + gcol;
+        } else {
+          const int xcol = c0 + scol[q];
+          const int iy = (int)yy * d.stride + (sop[q] == 1 ? dy0 : dy1);
+          const int ix = (int)xx * d.stride + (sop[q] == 1 ? dx0 : dx1);
+          if (xcol < d.Cx && (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)
+            src = d.x + (long long)im * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w + xcol;
+        }
+      }
+      floatx4v v = *(const floatx4v*)src;
+      if (XSQ && sop[q] != 0) v = v * v;
+      rs[q] = v;
+    }
+  };
+  auto sstore_q = [&](int buf, int q) {
+    if (!sok[q]) return;
+    __bf16* base = lds + buf * STAGE + sop[q] * OPER + srow[q] * PITCH + scol[q];
+    wg_bf16x4 vh, vm, vl;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      __bf16 hh, mm, ll;
+      split3_bf16(rs[q][e], hh, mm, ll);
+      vh[e] = hh; vm[e] = mm; vl[e] = ll;
+    }
+    *(wg_bf16x4*)base = vh;
+    *(wg_bf16x4*)(base + PLANE) = vm;
+    *(wg_bf16x4*)(base + 2 * PLANE) = vl;
+  };
+
+  const int ts = w >> 2, wq = w & 3, wm = wq >> 1, wn = wq & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int li = lane & 15;
+  const int tr_row = (8 * h + (li >> 2)) * PITCH;
+  const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  auto tr8 = [&](const __bf16* src) {
+    const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
+    const wg_bf16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
+    return (wg_bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  const bool active = ts == 0 || has1;  // wave-uniform
+
+  if (pb < pe) {
+    gload(pb);
+#pragma unroll
+    for (int q = 0; q < QP; ++q) sstore_q(0, q);
+    if (pb + BK < pe) gload(pb + BK);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (uint32_t p0 = pb; p0 < pe; p0 += BK) {
+    const __bf16* sb = lds + buf * STAGE;
+    const __bf16* xb = sb + (1 + ts) * OPER;
+    const bool more = p0 + BK < pe;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (active) {
+        wg_bf16x8 a[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE + tr_row + wm * WM + i * 32 + tr_col);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          wg_bf16x8 bq[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bq[q] = tr8(xb + q * PLANE + tr_row + wn * WN + j * 32 + tr_col);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bq[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[0], acc[i][j], 0, 0, 0);
+        }
+      }
+      // the next step's split + store behind this row group's MFMAs (slots 2i, 2i+1)
+      if (more) {
+        if (2 * i < QP) sstore_q(buf ^ 1, 2 * i);
+        if (2 * i + 1 < QP) sstore_q(buf ^ 1, 2 * i + 1);
+      }
+    }
+    if (more && p0 + 2 * BK < pe) gload(p0 + 2 * BK);
+    __syncthreads();
+    buf ^= 1;
+  }
+  static_assert(2 * TM >= QP, "every staged slot is stored behind some row group");
+
+  if (!active) return;
+  const int t = ts ? t1 : t0;
+  float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int gr = g0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (gr >= d.Cg) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = c0 + wn * WN + j * 32 + r;
+        if (col < d.ncols) slab[(long long)gr * d.ncols + col] = acc[i][j][reg];
+      }
+    }
+}
+
 struct WgRed {
   const float* partial;
   float* out;    // final [g][c][kk] (G == 1) or level-2 partial [G][g][t][c]
@@ -709,8 +902,20 @@ int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
 }
 
 int wg_x3_launch(const WgDesc& d, hipStream_t s) {
-  dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   const bool sq = d.x_op == AOP_SQUARE;
+  if (WG_X3_PAIR) {
+    dim3 gp((d.mtiles * d.ntiles * ((d.T + 1) / 2) * d.nsplit + 7) / 8 * 8);
+    if (d.rowfast) {
+      if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true, true>), gp, dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((wg_x3p_kernel<true, false>), gp, dim3(512), 0, s, d);
+    } else {
+      if (sq) hipLaunchKernelGGL((wg_x3p_kernel<false, true>), gp, dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((wg_x3p_kernel<false, false>), gp, dim3(512), 0, s, d);
+    }
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
+  dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
   if (d.rowfast) {
     if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true, TWO>), grid, dim3(256), 0, s, d);
@@ -834,7 +1039,8 @@ size_t wg_plan(WgDesc& d) {
   d.mtiles = ic_cdiv(d.Cg, d.bm);
   d.ntiles = ic_cdiv(d.ncols, d.bn);
   d.P = (long long)d.N * d.Hg * d.Wg;
-  const long long tiles = (long long)d.mtiles * d.ntiles * (d.generic ? 1 : d.T);
+  const long long tiles = (long long)d.mtiles * d.ntiles *
+                          (d.generic ? 1 : ((d.x3 && WG_X3_PAIR) ? (d.T + 1) / 2 : d.T));
   // one full wave of blocks: 256 CUs x 2 resident blocks = 512 slots, so a
   // grid of just over 512 equal blocks would run at half speed; never fewer
   // than 64 pixels per split
