@@ -17,6 +17,9 @@
 #ifndef IG_X3_M16
 #define IG_X3_M16 true  // ig_kernel_x3s on v_mfma_f32_16x16x32_bf16 (7-8 % faster than 32x32x16 on the conv fwd layers: DVFS holds a higher clock)
 #endif
+#ifndef IG_X3_BM256
+#define IG_X3_BM256 0  // > 0: 256-row 8-wave split tiles for maps with at least this many output pixels
+#endif
 #ifndef IG_X3_BM64
 #define IG_X3_BM64 0  // 1: 64-row tiles (3 blocks per CU) for every split-kernel layer
 #endif
@@ -660,13 +663,18 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
     }
 }
 
+// NT = 64 x (BM/WM) x (BN/WN) threads: 4 waves (128-row tiles, two blocks per
+// CU) or 8 waves (256-row tiles, one block per CU: each weight chunk staged
+// once per 256 output pixels)
 template <int BM, int BN, int WM, int WN, bool M16>
-__global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgDesc d) {
+__global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)) ig_kernel_x3s(const IgDesc d) {
   constexpr int LDB = 32;
   constexpr int WAVES_N = BN / WN;
-  constexpr int APASS = BM / 32, BPASS = BN / 64;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(BN % 64 == 0, "B staged 64 rows per pass");
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+  constexpr int APASS = BM * 8 / NT;              // A: 8 float4 per 32-channel row
+  constexpr int BSLOT = 3 * BN * 4;               // B: 4 x 16 B per 32-wide bf16 row, 3 planes
+  constexpr int BPASS = (BSLOT + NT - 1) / NT;
+  static_assert(BM * 8 % NT == 0, "whole A passes");
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * BM * LDB];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * BN * LDB];
 
@@ -687,13 +695,12 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
 
   const int tid = threadIdx.x;
   const int lrow = tid >> 3, lc4 = tid & 7;   // A: 8 float4 per 32-channel row
-  const int brow = tid >> 2, bq = tid & 3;    // B: 4 x 16 B per 32-wide bf16 row
   const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
   uint32_t a_off[APASS];
   int a_iy[APASS], a_ix[APASS];
 #pragma unroll
   for (int p = 0; p < APASS; ++p) {
-    const uint32_t m = m0 + lrow + 32 * p;
+    const uint32_t m = m0 + lrow + (NT / 8) * p;
     const bool ok = m < M;
     const uint32_t mm = ok ? m : 0u;
     const uint32_t img = fdiv(mm, P.fd_hw);
@@ -707,12 +714,26 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
   const float* __restrict__ xg = d.x;
   const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
   const size_t wplane = (size_t)d.wplane;
-  // swizzled store offsets (rows lrow + 32p / brow + 64p keep bits 2..3 of the row)
+  // swizzled store offsets (rows lrow + (NT/8) p keep bits 2..3 of the row)
   const int a_st = lrow * LDB + 8 * ((lc4 >> 1) ^ ig_swz(lrow)) + 4 * (lc4 & 1);
-  const int b_st = brow * LDB + 8 * (bq ^ ig_swz(brow));
+  // B: thread (brow, bq) stages 16-B chunk bq of (plane, row) pairs R = brow + (NT/4) p,
+  // plane R / BN, row R % BN; NT/4 is a multiple of 64, so every such row keeps
+  // bits 2..3 of brow and one swizzle serves all passes
+  const int brow = tid >> 2, bq = tid & 3;
+  const int b_sw = 8 * (bq ^ ig_swz(brow));
+  auto b_plane = [&](int p, int& q, int& row) {
+    if constexpr (NT == 256 && BN % 64 == 0) {  // compile-time plane / row block
+      q = p / (BN / 64);
+      row = brow + 64 * (p - q * (BN / 64));
+    } else {
+      const int R = brow + (NT / 4) * p;
+      q = R / BN;
+      row = R - q * BN;
+    }
+  };
 
   floatx4v ra[APASS];
-  bf16x8 rb[3][BPASS];
+  bf16x8 rb[BPASS];
   auto gload = [&](int c) {
     const int cc = c / P.T, t = c - cc * P.T;
     const int dy = P.dy[t], dx = P.dx[t];
@@ -724,11 +745,13 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
       const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;
       ra[p] = *(const floatx4v*)src;
     }
-    const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 32 + bq * 8;
+    const __bf16* wb = wpb + (size_t)t * d.Npad * d.Cin + cc * 32 + bq * 8;
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int p = 0; p < BPASS; ++p) rb[q][p] = *(const bf16x8*)(wb + q * wplane + (size_t)(64 * p) * d.Cin);
+    for (int p = 0; p < BPASS; ++p) {
+      int q, row;
+      b_plane(p, q, row);
+      if (BSLOT % NT == 0 || q < 3) rb[p] = *(const bf16x8*)(wb + q * wplane + (size_t)(n0 + row) * d.Cin);
+    }
   };
   const bool sq = d.a_op == AOP_SQUARE;  // GDN's x^2 (uniform)
   auto sstore = [&]() {
@@ -741,15 +764,17 @@ __global__ void __launch_bounds__(256, BM == 64 ? 3 : 2) ig_kernel_x3s(const IgD
         split3_bf16(sq ? ra[p][e] * ra[p][e] : ra[p][e], h, m, l);
         vh[e] = h; vm[e] = m; vl[e] = l;
       }
-      __bf16* dst = &As[a_st + 32 * p * LDB];
+      __bf16* dst = &As[a_st + (NT / 8) * p * LDB];
       *(bf16x4*)dst = vh;
       *(bf16x4*)(dst + BM * LDB) = vm;
       *(bf16x4*)(dst + 2 * BM * LDB) = vl;
     }
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[q * BN * LDB + b_st + 64 * p * LDB] = rb[q][p];
+    for (int p = 0; p < BPASS; ++p) {
+      int q, row;
+      b_plane(p, q, row);
+      if (BSLOT % NT == 0 || q < 3) *(bf16x8*)&Bs[(q * BN + row) * LDB + b_sw] = rb[p];
+    }
   };
 
   const int lane = tid & 63, w = tid >> 6;
@@ -1068,7 +1093,12 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
   dim3 grid(mt, d.Npad / BN, d.nphase * d.ksplit);
   const bool sq = d.a_op == AOP_SQUARE;
-  if (d.bf16) {
+  if constexpr ((BM / WM) * (BN / WN) == 8) {  // 8-wave tiles: split kernel only
+    if (!d.x3) return IC_ERR_ARG;
+    hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, IG_X3_M16>), grid, dim3(512), 0, s, d);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  } else if (d.bf16) {
     if (sq) return IC_ERR_ARG;
     hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
   } else if (d.x3) {
@@ -1115,6 +1145,8 @@ size_t ig_plan(IgDesc& d) {
     // small maps (hyperprior and <= 32x32 at batch 32): 64-row tiles double the tile
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
     d.bm = (!d.bf16 && (mall < 65536 || (IG_X3_BM64 && d.x3))) ? 64 : 128;
+    // split kernel on large maps: 256-row, 8-wave tiles (weights staged once per 256 pixels)
+    if (IG_X3_BM256 && d.x3 && IG_X3_REG == 2 && mall >= IG_X3_BM256) d.bm = 256;
     d.bn = 192;
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
@@ -1164,7 +1196,8 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
-  if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
+  if (d.bn == 192 && d.bm == 256) rc = ig_launch_t<256, 192, 64, 96>(d, s);
+  else if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
   else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);
   else rc = ig_launch_t<256, 32, 64, 32>(d, s);
