@@ -56,11 +56,12 @@ CONFIGS = {
                gflop=73.70),
 }
 MATH_NOTE = {
-    "fp32_split": "fp32 via exact 3-term bf16 operand split, 6 products on v_mfma_f32_32x32x16_bf16, fp32 "
-                  "accumulation (fp32 fma-chain error; wide conv fwd/dgrad); weight gradients, GDN, entropy "
-                  "models, edges on the fp32 MFMA / VALU",
+    "fp32_split": "fp32 via exact 3-term bf16 operand split, 6 products on v_mfma_f32_16x16x32_bf16, fp32 "
+                  "accumulation (fp32 fma-chain error): wide conv fwd/dgrad/wgrad, GDN (C=192) fwd and dgamma; "
+                  "entropy models and the 3-channel edges on the fp32 MFMA / VALU",
     "fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain)",
-    "bf16": "bf16 operands, fp32 accumulation (g_a/g_s conv fwd/dgrad); rest fp32",
+    "bf16": "bf16 operands, fp32 accumulation (g_a/g_s conv fwd/dgrad); weight gradients, hyperprior and GDN "
+            "in fp32_split; entropy models and edges fp32",
 }
 BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
 
@@ -107,7 +108,7 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     achieved = flop / (ms * 1e-3) / 1e12
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
-        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,true> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
+        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,true,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
     else:
         peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",

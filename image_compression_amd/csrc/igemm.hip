@@ -14,6 +14,12 @@
 #ifndef IG_X3_REG
 #define IG_X3_REG 2  // split kernel: 2 swizzled register-staged (ig_kernel_x3s), 1 padded (ig_kernel_x3), 0 LDS-DMA (ig_kernel_x3d); 2 measured fastest
 #endif
+#ifndef IG_BF16_S
+// bf16 operands on small maps (64-row tiles) on ig_kernel_x3s's swizzled 16x16x32
+// structure, one product: 0.056 vs 0.072-0.080 ms on g_a.6 / g_s.0 (the padded
+// 64-channel-chunk kernel keeps the 128-row tiles: 0.378 vs 0.412 ms on g_a.2)
+#define IG_BF16_S 1
+#endif
 #ifndef IG_X3_M16
 #define IG_X3_M16 true  // ig_kernel_x3s on v_mfma_f32_16x16x32_bf16 (7-8 % faster than 32x32x16 on the conv fwd layers: DVFS holds a higher clock)
 #endif
@@ -666,17 +672,20 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
 // NT = 64 x (BM/WM) x (BN/WN) threads: 4 waves (128-row tiles, two blocks per
 // CU) or 8 waves (256-row tiles, one block per CU: each weight chunk staged
 // once per 256 output pixels)
-template <int BM, int BN, int WM, int WN, bool M16>
+// NP = 3: the exact split (six products); NP = 1: plain bf16 operands (RN of
+// the activations, bf16-packed weights) with fp32 accumulation, one product
+template <int BM, int BN, int WM, int WN, bool M16, int NP = 3>
 __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)) ig_kernel_x3s(const IgDesc d) {
+  static_assert(NP == 3 || (NP == 1 && M16), "bf16 mode on the 16x16x32 MFMA only");
   constexpr int LDB = 32;
   constexpr int WAVES_N = BN / WN;
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
   constexpr int APASS = BM * 8 / NT;              // A: 8 float4 per 32-channel row
-  constexpr int BSLOT = 3 * BN * 4;               // B: 4 x 16 B per 32-wide bf16 row, 3 planes
+  constexpr int BSLOT = NP * BN * 4;              // B: 4 x 16 B per 32-wide bf16 row, NP planes
   constexpr int BPASS = (BSLOT + NT - 1) / NT;
   static_assert(BM * 8 % NT == 0, "whole A passes");
-  __shared__ __attribute__((aligned(16))) __bf16 As[3 * BM * LDB];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * BN * LDB];
+  __shared__ __attribute__((aligned(16))) __bf16 As[NP * BM * LDB];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NP * BN * LDB];
 
   const int zi = blockIdx.z;
   const int phase = zi / d.ksplit;
@@ -750,13 +759,20 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
     for (int p = 0; p < BPASS; ++p) {
       int q, row;
       b_plane(p, q, row);
-      if (BSLOT % NT == 0 || q < 3) rb[p] = *(const bf16x8*)(wb + q * wplane + (size_t)(n0 + row) * d.Cin);
+      if (BSLOT % NT == 0 || q < NP) rb[p] = *(const bf16x8*)(wb + q * wplane + (size_t)(n0 + row) * d.Cin);
     }
   };
   const bool sq = d.a_op == AOP_SQUARE;  // GDN's x^2 (uniform)
   auto sstore = [&]() {
 #pragma unroll
     for (int p = 0; p < APASS; ++p) {
+      if constexpr (NP == 1) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (__bf16)ra[p][e];
+        *(bf16x4*)&As[a_st + (NT / 8) * p * LDB] = v;
+        continue;
+      }
       bf16x4 vh, vm, vl;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -773,7 +789,7 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
     for (int p = 0; p < BPASS; ++p) {
       int q, row;
       b_plane(p, q, row);
-      if (BSLOT % NT == 0 || q < 3) *(bf16x8*)&Bs[(q * BN + row) * LDB + b_sw] = rb[p];
+      if (BSLOT % NT == 0 || q < NP) *(bf16x8*)&Bs[(q * BN + row) * LDB + b_sw] = rb[p];
     }
   };
 
@@ -798,18 +814,22 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
     const __bf16* Brd = &Bs[(wn * WN + r) * LDB + ch];
     for (int c = cb; c < ce; ++c) {
       if (c + 1 < ce) gload(c + 1);
-      bf16x8 a[3][TM];
+      bf16x8 a[NP][TM];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NP; ++q)
 #pragma unroll
         for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 16) * LDB);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bf16x8 b[3];
+        bf16x8 b[NP];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
+        for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
+          if constexpr (NP == 1) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+            continue;
+          }
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
@@ -1100,6 +1120,14 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
     return IC_OK;
   } else if (d.bf16) {
     if (sq) return IC_ERR_ARG;
+    if constexpr (BN % 64 == 0 && BM == 64) {
+      if (IG_BF16_S) {
+        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, true, 1>), grid, dim3(256), 0, s, d);
+        IC_CHECK_LAUNCH();
+        return IC_OK;
+      }
+    }
+    if (BM == 64) return IC_ERR_ARG;
     hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
   } else if (d.x3) {
     if constexpr (BN % 64 == 0) {
@@ -1128,6 +1156,10 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
 
 }  // namespace
 
+// bf16 operands on the padded 64-channel-chunk kernel (ig_kernel_bf16) rather
+// than the swizzled 32-channel one (ig_kernel_x3s<..., 1>)
+static bool ig_bf16_wide(const IgDesc& d) { return d.bf16 && !(IG_BF16_S && d.bn % 64 == 0 && d.bm == 64); }
+
 int ig_npad(int Cout) {
   if (Cout % 192 == 0) return Cout;
   if (Cout >= 64) return (Cout + 63) / 64 * 64;
@@ -1144,7 +1176,7 @@ size_t ig_plan(IgDesc& d) {
   if (d.Cout % 192 == 0) {
     // small maps (hyperprior and <= 32x32 at batch 32): 64-row tiles double the tile
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
-    d.bm = (!d.bf16 && (mall < 65536 || (IG_X3_BM64 && d.x3))) ? 64 : 128;
+    d.bm = ((!d.bf16 || IG_BF16_S) && (mall < 65536 || (IG_X3_BM64 && d.x3))) ? 64 : 128;
     // split kernel on large maps: 256-row, 8-wave tiles (weights staged once per 256 pixels)
     if (IG_X3_BM256 && d.x3 && IG_X3_REG == 2 && mall >= IG_X3_BM256) d.bm = 256;
     d.bn = 192;
@@ -1166,7 +1198,7 @@ size_t ig_plan(IgDesc& d) {
     mtot += M;
     tiles += (long long)P.mtiles * (d.Npad / d.bn);
     const int nch = d.generic ? (d.Kc >> 5)
-                  : P.T * (d.bf16 ? (d.Cin >> 6) : (d.x3 && IG_X3_REG == 0) ? (d.Cin >> 4) : (d.Cin >> 5));
+                  : P.T * (ig_bf16_wide(d) ? (d.Cin >> 6) : (d.x3 && IG_X3_REG == 0) ? (d.Cin >> 4) : (d.Cin >> 5));
     nchunks_max = nch > nchunks_max ? nch : nchunks_max;
   }
   d.Mtot = mtot;
@@ -1192,7 +1224,7 @@ size_t ig_plan(IgDesc& d) {
 int ig_run(IgDesc& d, hipStream_t s) {
   if (d.Mtot == 0) return IC_OK;
   if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
-  if (d.bf16 && (d.generic || d.Cin % 64 != 0)) return IC_ERR_ARG;
+  if (d.bf16 && (d.generic || (ig_bf16_wide(d) && d.Cin % 64 != 0))) return IC_ERR_ARG;
   if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
