@@ -99,8 +99,11 @@ __device__ __forceinline__ int edge_koff(const EdgeGeom& g, int k, int zero_off,
 
 // ------------------------------------------------------------------ conv
 // y NHWC (channel stride 1, pixel stride ys_w), Cout = 64*NTW*... : wave slice = Cout/4
+#ifndef EDGE_CONV_PER_CU
+#define EDGE_CONV_PER_CU 2
+#endif
 template <int COUT>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
     edge_conv_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
                      int relu, float* __restrict__ y, long long ys_n, long long ys_h, long long ys_w) {
   constexpr int NTW = COUT / 64;
@@ -477,7 +480,7 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
   if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
   // 16-B channel-quad stores
   if (ys_c != 1 || Kp < g.TC || ((uintptr_t)y & 15) || ys_w % 4 || ys_h % 4 || ys_n % 4) return IC_ERR_ARG;
-  const int grid = edge_grid(g.units, 2);
+  const int grid = edge_grid(g.units, EDGE_CONV_PER_CU);
   if (grid < 1) return IC_OK;
   switch (Cout) {
     case 192:

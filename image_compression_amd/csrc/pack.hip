@@ -67,6 +67,23 @@ __global__ void pack_kernel(const PackArgs p) {
     store_packed(p, i, total, v);
   }
 }
+// fast layouts (mode 0 / 1, not generic): tap t = blockIdx.y, one thread per
+// (n, r) of it; 32-bit index arithmetic (the generic kernel's 64-bit divisions
+// dominated its time)
+__global__ void pack_fast_kernel(const PackArgs p) {
+  const int Nout = p.mode == 0 ? p.A : p.B;
+  const uint32_t R = (uint32_t)(p.mode == 0 ? p.B : p.A);
+  const uint32_t nr = (uint32_t)p.Npad * R;
+  const uint32_t total = (uint32_t)p.T * nr;
+  const int t = blockIdx.y;
+  const int toff = p.ky[t] * p.k + p.kx[t], kk = p.k * p.k;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += gridDim.x * blockDim.x) {
+    const uint32_t n = i / R, r = i - n * R;
+    float v = 0.f;
+    if ((int)n < Nout) v = p.W[(p.mode == 0 ? n * (uint32_t)p.B + r : r * (uint32_t)p.B + n) * (uint32_t)kk + toff];
+    store_packed(p, (long long)((uint32_t)t * nr + i), (long long)total, v);
+  }
+}
 }  // namespace
 
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int T, const int* ky,
@@ -78,6 +95,14 @@ int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int
   for (int t = 0; t < T; ++t) { p.ky[t] = ky[t]; p.kx[t] = kx[t]; }
   const int R = mode == 0 ? B : A;
   const long long total = mode == 2 ? (long long)Npad * A : (generic ? (long long)Npad * Kpad : (long long)T * Npad * R);
+  if (!generic && mode < 2 && total < (1ll << 31)) {
+    const long long nr = (long long)Npad * R;
+    long long blocks = (nr + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(pack_fast_kernel, dim3((unsigned)blocks, T), dim3(256), 0, s, p);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   long long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);

@@ -985,16 +985,21 @@ __global__ void __launch_bounds__(256) colsum_rows_kernel(const float* t, long l
   const long long r0 = (long long)blockIdx.x * rpb;
   long long r1 = r0 + rpb;
   if (r1 > rows) r1 = rows;
-  floatx4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  floatx4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
   if (g < groups) {
     const float* base = t + (size_t)c4 * 4;
     long long r = r0 + g;
-    for (; r + groups < r1; r += 2 * groups) {
-      acc0 += *(const floatx4v*)(base + (size_t)r * C);
-      acc1 += *(const floatx4v*)(base + (size_t)(r + groups) * C);
+    for (; r + 3 * groups < r1; r += 4 * groups) {  // four 16-B loads in flight per thread
+      const floatx4v v0 = *(const floatx4v*)(base + (size_t)r * C);
+      const floatx4v v1 = *(const floatx4v*)(base + (size_t)(r + groups) * C);
+      const floatx4v v2 = *(const floatx4v*)(base + (size_t)(r + 2 * groups) * C);
+      const floatx4v v3 = *(const floatx4v*)(base + (size_t)(r + 3 * groups) * C);
+      acc0 += v0; acc1 += v1; acc2 += v2; acc3 += v3;
     }
-    if (r < r1) acc0 += *(const floatx4v*)(base + (size_t)r * C);
+    for (; r < r1; r += groups) acc0 += *(const floatx4v*)(base + (size_t)r * C);
     acc0 += acc1;
+    acc2 += acc3;
+    acc0 += acc2;
     *(floatx4v*)&lds[(g * c4n + c4) * 4] = acc0;
   }
   __syncthreads();

@@ -9,7 +9,7 @@ C=$R/image_compression_amd/csrc
 B=$R/tools/_abl/build_$TAG
 mkdir -p $B
 for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics; do
-  if [ "$f" = "igemm" ] || [ "$f" = "wgrad" ] || [ "$f" = "gdn_fused" ] || [ ! -f $B/$f.o ]; then
+  if [ "$f" = "igemm" ] || [ "$f" = "wgrad" ] || [ "$f" = "gdn_fused" ] || [ "$f" = "edge" ] || [ ! -f $B/$f.o ]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C "$@" -c $C/$f.hip -o $B/$f.o &
   fi
 done

@@ -24,7 +24,7 @@ ONLY = None
 
 
 def t_ms(fn, reps, tag=None):
-    if ONLY is not None and tag is not None and ONLY not in tag:
+    if ONLY is not None and tag is not None and not any(o in tag for o in ONLY.split(",")):
         return float("nan")
     fn()
     torch.cuda.synchronize()
@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default=None, help="run only ops whose 'layer op' contains this text")
+    ap.add_argument("--only", default=None, help="run only ops whose 'layer op' contains this text (comma-separated alternatives)")
     ap.add_argument("--math", type=int, default=0, help="IC_MATH_* of the conv fwd / dgrad / wgrad (0 fp32, 2 fp32 split)")
     ap.add_argument("--gdn-math", type=int, default=0, help="IC_MATH_* of the GDN forward")
     a = ap.parse_args()
