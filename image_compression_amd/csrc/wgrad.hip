@@ -407,6 +407,9 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 // TWO: two blocks per CU — unpadded 192-bf16 rows whose 16-B chunks are
 // XOR-swizzled by 4 on rows with bit 1 set (the four rows of a transposed read
 // then start 0 / 32 / 16 / 48 dwords apart mod 64), 74 KB of LDS per block.
+#ifndef WG_X3_ABL
+#define WG_X3_ABL 0  // timing ablations (results invalid): 1 no global loads, 2 no split, 4 no split/LDS stores, 8 no barrier
+#endif
 template <bool ROWFAST, bool XSQ, bool TWO>
 __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d) {
   constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
@@ -449,7 +452,19 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 
   // two register sets: a step's global loads are issued two steps before its split + store
   floatx4v g0r[QP], x0r[QP], g1r[QP], x1r[QP];
-  auto gload = [&](uint32_t p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+  // live == false (a refill past the split) still issues every load, from the
+  // zero page: with the loads unconditional the compiler's vmcnt bookkeeping
+  // keeps both register sets in flight (a branch around them made it drain all
+  // loads, vmcnt(0), one step after they were issued)
+  auto gload = [&](uint32_t p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP], bool live = true) {
+    if (WG_X3_ABL & 1) {  // ablation: no global loads
+#pragma unroll
+      for (int q = 0; q < QP; ++q) {
+        rg[q] = floatx4v{(float)p0, 1.f, 2.f, 3.f};
+        rx[q] = floatx4v{(float)(p0 + q), 1.f, 2.f, 3.f};
+      }
+      return;
+    }
     if (ROWFAST) {
       // a 16-pixel step never crosses an output row: image / row / first column are uniform
       const uint32_t img = fdiv(p0, d.fd_hw);
@@ -458,14 +473,14 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
       const uint32_t gx0 = rr - gy * d.fd_w.d;
       const float* gb = d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w;
       const int iy = (int)gy * d.stride + dyt, ix0 = (int)gx0 * d.stride + dxt;
-      const bool rowok = (unsigned)iy < (unsigned)d.Hx;
+      const bool rowok = live && (unsigned)iy < (unsigned)d.Hx;
       const float* xb = d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h;
 #pragma unroll
       for (int q = 0; q < QP; ++q) {
         // branch-free: padding and out-of-range columns read a zero page
         const int gcol = g0 + scol[q], xcol = c0 + scol[q];
         const int ix = ix0 + srow[q] * d.stride;
-        const float* gs = gcol < d.Cg ? gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
+        const float* gs = (live && gcol < d.Cg) ? gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
         const float* xs = (rowok && xcol < d.Cx && (unsigned)ix < (unsigned)d.Wx)
                               ? xb + (long long)ix * d.xs_w + xcol : wg_zero_page;
         rg[q] = *(const floatx4v*)gs;
@@ -479,7 +494,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
     for (int q = 0; q < QP; ++q) {
       const uint32_t p = p0 + srow[q];
       floatx4v vg = {0.f, 0.f, 0.f, 0.f}, vx = {0.f, 0.f, 0.f, 0.f};
-      if (p < pe) {
+      if (live && p < pe) {
         const uint32_t img = fdiv(p, d.fd_hw);
         const uint32_t rr = p - img * d.fd_hw.d;
         const uint32_t gy = fdiv(rr, d.fd_w);
@@ -502,6 +517,10 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
   // split + store one staged float4 of each operand (q), so the store pass can
   // be spread between the MFMA groups of the previous step
   auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
+    if (WG_X3_ABL & 4) {  // ablation: no split, no LDS stores (keep the loads live)
+      if (rg[q][0] == 12345.f && rx[q][1] == 54321.f) lds[tid] = (__bf16)rg[q][2];
+      return;
+    }
     __bf16* base = lds + buf * STAGE;
 #pragma unroll
     for (int op = 0; op < 2; ++op) {
@@ -510,7 +529,11 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         __bf16 hh, mm, ll;
-        split3_bf16(v[e], hh, mm, ll);
+        if (WG_X3_ABL & 2) {  // ablation: no split arithmetic
+          hh = mm = ll = (__bf16)v[e];
+        } else {
+          split3_bf16(v[e], hh, mm, ll);
+        }
         vh[e] = hh; vm[e] = mm; vl[e] = ll;
       }
       __bf16* dst = base + op * OPER + srow[q] * PITCH + (scol[q] ^ (TWO ? ((srow[q] >> 1) & 1) << 5 : 0));
@@ -591,8 +614,9 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
       }
     }
     // refill the set just stored: DEPTH steps ahead (never past the split: row-fast loads are unmasked)
-    if (p0 + (DEPTH + 1) * BK < (int)pe) gload((uint32_t)(p0 + (DEPTH + 1) * BK), rg, rx);
-    __syncthreads();
+    if (ROWFAST || p0 + (DEPTH + 1) * BK < (int)pe)
+      gload((uint32_t)(p0 + (DEPTH + 1) * BK), rg, rx, p0 + (DEPTH + 1) * BK < (int)pe);
+    if (!(WG_X3_ABL & 8)) __syncthreads();
   };
 
   // steps run in pairs (with DEPTH 2 the two register sets alternate
@@ -612,8 +636,10 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
       gload((uint32_t)q0, g0r, x0r);
     }
     sstore(0, g0r, x0r);
-    if (q0 + BK < (int)pe) gload((uint32_t)(q0 + BK), g1s, x1s);
-    if (DEPTH == 2 && q0 + 2 * BK < (int)pe) gload((uint32_t)(q0 + 2 * BK), g0r, x0r);
+    // unconditional (ROWFAST): every path into the loop then has the same loads in flight
+    if (ROWFAST || q0 + BK < (int)pe) gload((uint32_t)(q0 + BK), g1s, x1s, q0 + BK < (int)pe);
+    if (DEPTH == 2 && (ROWFAST || q0 + 2 * BK < (int)pe))
+      gload((uint32_t)(q0 + 2 * BK), g0r, x0r, q0 + 2 * BK < (int)pe);
   }
   __syncthreads();
   for (int p0 = q0; p0 < (int)pe; p0 += 2 * BK) {
