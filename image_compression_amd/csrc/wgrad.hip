@@ -410,12 +410,15 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef WG_X3_ABL
 #define WG_X3_ABL 0  // timing ablations (results invalid): 1 no global loads, 2 no split, 4 no split/LDS stores, 8 no barrier
 #endif
+#ifndef WG_X3_DEPTH
+#define WG_X3_DEPTH 2  // steps of global loads in flight ahead of their split + store (2 or 3)
+#endif
 template <bool ROWFAST, bool XSQ, bool TWO>
 __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d) {
   constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int PITCH = TWO ? 192 : 224;    // bf16 per image row
-  constexpr int DEPTH = TWO ? 1 : 2;        // register sets of staged loads in flight
+  constexpr int DEPTH = TWO ? 1 : WG_X3_DEPTH;  // register sets of staged loads in flight
   constexpr int PLANE = BK * PITCH;         // one part of one operand
   constexpr int OPER = 3 * PLANE;           // three parts
   constexpr int STAGE = 2 * OPER;           // G and X
@@ -451,7 +454,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
   }
 
   // two register sets: a step's global loads are issued two steps before its split + store
-  floatx4v g0r[QP], x0r[QP], g1r[QP], x1r[QP];
+  floatx4v g0r[QP], x0r[QP], g1r[QP], x1r[QP], g2r[QP], x2r[QP];  // g2r/x2r: DEPTH 3 only
   // live == false (a refill past the split) still issues every load, from the
   // zero page: with the loads unconditional the compiler's vmcnt bookkeeping
   // keeps both register sets in flight (a branch around them made it drain all
@@ -621,9 +624,31 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 
   // steps run in pairs (with DEPTH 2 the two register sets alternate
   // statically); an odd count is padded with one all-zero step in front
+  const int nsteps = pe > pb ? (int)((pe - pb + BK - 1) / BK) : 0;
+  if constexpr (DEPTH == 3) {
+    // three register sets rotate over steps in threes (LDS buffers alternate, so
+    // the group's first buffer flips each group); the count is padded to a
+    // multiple of three with all-zero steps in front (zero-page loads)
+    const int q3 = (int)pb - ((3 - nsteps % 3) % 3) * BK;
+    auto live = [&](int p) { return p >= (int)pb && p < (int)pe; };
+    if (nsteps > 0) {
+      gload((uint32_t)q3, g0r, x0r, live(q3));
+      sstore(0, g0r, x0r);
+      gload((uint32_t)(q3 + BK), g1r, x1r, live(q3 + BK));
+      gload((uint32_t)(q3 + 2 * BK), g2r, x2r, live(q3 + 2 * BK));
+      gload((uint32_t)(q3 + 3 * BK), g0r, x0r, live(q3 + 3 * BK));
+    }
+    __syncthreads();
+    int b = 0;
+    for (int p0 = q3; p0 < (int)pe; p0 += 3 * BK) {
+      step(p0, b, g1r, x1r);
+      step(p0 + BK, b ^ 1, g2r, x2r);
+      step(p0 + 2 * BK, b, g0r, x0r);
+      b ^= 1;
+    }
+  } else {
   auto& g1s = DEPTH == 2 ? g1r : g0r;
   auto& x1s = DEPTH == 2 ? x1r : x0r;
-  const int nsteps = pe > pb ? (int)((pe - pb + BK - 1) / BK) : 0;
   const int q0 = (int)pb - ((nsteps & 1) ? BK : 0);
   if (nsteps > 0) {
     if (nsteps & 1) {
@@ -645,6 +670,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
   for (int p0 = q0; p0 < (int)pe; p0 += 2 * BK) {
     step(p0, 0, g1s, x1s);
     step(p0 + BK, 1, g0r, x0r);
+  }
   }
 
   float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
