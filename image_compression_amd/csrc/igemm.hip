@@ -14,6 +14,9 @@
 #ifndef IG_X3_REG
 #define IG_X3_REG 2  // split kernel: 2 swizzled register-staged (ig_kernel_x3s), 1 padded (ig_kernel_x3), 0 LDS-DMA (ig_kernel_x3d); 2 measured fastest
 #endif
+#ifndef IG_X3S_ABL
+#define IG_X3S_ABL 0  // timing ablations of ig_kernel_x3s (results invalid): 1 no global loads, 4 no split/LDS store/barriers
+#endif
 #ifndef IG_BF16_S
 // bf16 operands on small maps (64-row tiles) on ig_kernel_x3s's swizzled 16x16x32
 // structure, one product: 0.056 vs 0.072-0.080 ms on g_a.6 / g_s.0 (the padded
@@ -744,6 +747,13 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   floatx4v ra[APASS];
   bf16x8 rb[BPASS];
   auto gload = [&](int c) {
+    if (IG_X3S_ABL & 1) {  // ablation: no global loads
+#pragma unroll
+      for (int p = 0; p < APASS; ++p) ra[p] = floatx4v{(float)c, 1.f, 2.f, 3.f};
+#pragma unroll
+      for (int p = 0; p < BPASS; ++p) rb[p] = bf16x8{};
+      return;
+    }
     const int cc = c / P.T, t = c - cc * P.T;
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
@@ -837,6 +847,10 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
         }
+      }
+      if (IG_X3S_ABL & 4) {  // ablation: no split / LDS store / barriers (keep the loads live)
+        if (ra[0][0] == 12345.f) As[tid] = (__bf16)ra[0][1];
+        continue;
       }
       __syncthreads();
       if (c + 1 < ce) sstore();
