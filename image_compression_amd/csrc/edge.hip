@@ -376,6 +376,9 @@ int edge_grid(long long units, int per_cu) {
 // MFMA step s = 4u + v consumes channel 16u + 4lq + v on both sides, so a
 // lane's A operand is one float4 of its pixel's channels.
 constexpr int TF_KY = 3;  // taps per parity for k <= 5
+#ifndef TCONV_FEW2
+#define TCONV_FEW2 1  // stride-2 upsampling to few channels on the input-row-stationary kernel (Win <= 128)
+#endif
 
 template <int NWV, int MTW>  // waves, 16-pixel m-tiles per wave: input width <= 16 * NWV * MTW
 __global__ void __launch_bounds__(64 * NWV, 2)
@@ -469,6 +472,140 @@ __global__ void __launch_bounds__(64 * NWV, 2)
       }
     }
   }
+}
+// Input-row-stationary variant (stride 2, input width <= 16 * NWV): each
+// block walks a run of input rows of one image; every input row is loaded
+// once (one float4 of 16 channels per lane, all channels in flight, the next
+// row prefetched into a second register set during this row's MFMAs) and
+// multiplied by the weights of all k tap rows (k 16-column MFMA tiles: col =
+// (kx, o)).  Tap row ky of input row r belongs to output row Y = 2r - pad + ky
+// and lands in that row's slot of an LDS ring of pending output rows: the
+// row's first contribution (ky = k - 1 or k - 2, by parity) stores, later
+// ones add, in input-row order.  After input row r the rows 2r - pad and
+// 2r - pad + 1 are complete; they are gathered (fixed order, kx ascending) and
+// written during the next row's MFMAs, one barrier per input row.  A block
+// starts (k - 1) / 2 rows before its run (halo: nothing emitted), and rows
+// outside the image still store zeros, so every emitted row is exact.  Input
+// traffic ~1.1x the tensor (vs ~2.5x for the output-row-stationary kernel).
+constexpr int TF2_RS = 8;  // ring slots: rows 2r - pad - 2 .. 2r - pad + k - 1 in flight
+
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1)
+    tconv_few2_kernel(const float* __restrict__ x, int N, int Hin, int Win, int Cin, const float* __restrict__ W,
+                      int Cout, int k, int pad, const float* __restrict__ bias, int relu, float* __restrict__ y,
+                      long long ysn, long long ysc, long long ysh, long long ysw, int Hout, int Wout, int run) {
+  constexpr int WMAX = 16 * NWV;
+  constexpr int NT = 64 * NWV;
+  __shared__ __attribute__((aligned(16))) float wl[5 * 12 * 4 * 16 * 4];  // [ky][u][q][col][v], Cin <= 192
+  __shared__ __attribute__((aligned(16))) float ring[TF2_RS * WMAX * 16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int U = Cin >> 4;
+  const int ncol = k * Cout;
+  for (int i = tid; i < k * U * 4 * 16 * 4; i += NT) {
+    const int v = i & 3, col = (i >> 2) & 15, q = (i >> 6) & 3, rr = i >> 8;
+    const int u = rr % U, ky = rr / U;
+    const int c = 16 * u + 4 * q + v;
+    float val = 0.f;
+    if (col < ncol) {
+      const int kx = col / Cout, o = col - (col / Cout) * Cout;
+      val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
+    }
+    wl[i] = val;
+  }
+  __syncthreads();
+
+  const int nrun = (Hin + run - 1) / run;
+  const int n = blockIdx.x / nrun;
+  const int r0 = (blockIdx.x - n * nrun) * run;
+  const bool last = r0 + run >= Hin;
+  const int rlast = last ? (Hout - 1 + pad) >> 1 : r0 + run - 1;   // last input row whose rows are emitted
+  const int rfirst = r0 - (k - 1) / 2;
+  const int px = 16 * w + li;
+  const float* xn = x + (size_t)n * Hin * Win * Cin;
+
+  floatx4v a0[12], a1[12];
+  auto load = [&](int r, floatx4v (&a)[12]) {
+    const bool ok = r >= 0 && r < Hin && px < Win;
+    const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? px : 0)) * Cin + 4 * lq;
+#pragma unroll
+    for (int u = 0; u < 12; ++u)
+      a[u] = (ok && u < U) ? *(const floatx4v*)(xr + 16 * u) : floatx4v{0.f, 0.f, 0.f, 0.f};
+  };
+  // the two rows completed by input row r (emitted from the block's run on)
+  auto emit = [&](int r) {
+    if (r < r0) return;
+    for (int h = 0; h < 2; ++h) {
+      const int Y = 2 * r - pad + h;
+      if (Y < 0 || Y >= Hout) continue;
+      const float* sl = ring + (Y & (TF2_RS - 1)) * WMAX * 16;
+      for (int X = tid; X < Wout; X += NT) {
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int kx = (X + pad) & 1; kx < k; kx += 2) {
+          const int ix = (X + pad - kx) >> 1;
+          if (ix < 0 || ix >= Win) continue;
+          const float* cp = sl + ix * 16 + kx * Cout;
+          for (int o = 0; o < Cout; ++o) sum[o] += cp[o];
+        }
+        for (int o = 0; o < Cout; ++o) {
+          float v = sum[o] + (bias ? bias[o] : 0.f);
+          if (relu) v = v > 0.f ? v : 0.f;
+          y[n * ysn + o * ysc + (long long)Y * ysh + (long long)X * ysw] = v;
+        }
+      }
+    }
+  };
+  // one input row: its k tap-row tiles (MFMAs), the previous row's completed
+  // rows emitted meanwhile, then the tiles stored / added into the ring
+  auto row = [&](int r, const floatx4v (&a)[12]) {
+    floatx4v acc[5];
+#pragma unroll
+    for (int ky = 0; ky < 5; ++ky) acc[ky] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    if (r >= 0 && r < Hin) {
+#pragma unroll
+      for (int u = 0; u < 12; ++u) {
+        if (u < U) {
+#pragma unroll
+          for (int ky = 0; ky < 5; ++ky) {
+            if (ky < k) {
+              const floatx4v b4 = *(const floatx4v*)(wl + ((((ky * U + u) * 4 + lq) * 16 + li) << 2));
+#pragma unroll
+              for (int v = 0; v < 4; ++v)
+                acc[ky] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][v], b4[v], acc[ky], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    emit(r - 1);  // its slots are not written by this row (ring of 8)
+    // C/D map: pixel 16w + 4lq + e, column li; each (pixel, column) of a slot has one owner
+#pragma unroll
+    for (int ky = 0; ky < 5; ++ky) {
+      const int Y = 2 * r - pad + ky;
+      if (ky < k && Y >= 0 && Y < Hout) {
+        float* sl = ring + ((Y & (TF2_RS - 1)) * WMAX + 16 * w + 4 * lq) * 16 + li;
+        if (ky >= k - 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sl[16 * e] = acc[ky][e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sl[16 * e] += acc[ky][e];
+        }
+      }
+    }
+    __syncthreads();  // this row's ring writes before the next row's emission; emission reads before reuse
+  };
+
+  load(rfirst, a0);
+  int r = rfirst;
+  for (; r <= rlast; r += 2) {
+    load(r + 1, a1);
+    row(r, a0);
+    if (r + 1 > rlast) { ++r; break; }
+    load(r + 2, a0);
+    row(r + 1, a1);
+  }
+  emit(rlast);
 }
 }  // namespace
 
@@ -570,6 +707,17 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
                   const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
                   int Hout, int Wout, hipStream_t s) {
   if (((uintptr_t)x & 15) || Hout < 1 || Wout < 1) return IC_ERR_ARG;
+  if (TCONV_FEW2 && Win <= 128 && k <= 5 && (Hout - 1 + pad) / 2 <= Hin + 2) {
+    // input-row stationary: runs of input rows, about one block per CU
+    long long run = ((long long)N * Hin + 255) / 256;
+    if (run < 4) run = 4;
+    if (run > Hin) run = Hin;
+    const long long blocks = (long long)N * ((Hin + run - 1) / run);
+    hipLaunchKernelGGL((tconv_few2_kernel<8>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W, Cout,
+                       k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   const long long rows = (long long)N * ((Hout + 1) / 2);
   long long grid = 2 * (rows < 256 ? rows : 256);  // two parities, <= 2 blocks per CU
   if (Win <= 64)

@@ -75,6 +75,7 @@ TCONV_CASES = [
     (1, 16, 2, 130, 3, 3, 2, 1, 1),    # 4 m-tiles per wave, k = 3
     (1, 48, 6, 5, 4, 3, 2, 1, 1),      # Cout = 4
     (1, 32, 5, 5, 3, 5, 2, 2, 0),      # odd output height (no output padding)
+    (3, 192, 20, 24, 3, 5, 2, 2, 1),   # input-row-stationary kernel: several runs per image, halo rows
     (1, 96, 5, 7, 64, 5, 2, 2, 1),
     (2, 320, 4, 4, 192, 5, 2, 2, 1),
 ]
