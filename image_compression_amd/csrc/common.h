@@ -56,6 +56,46 @@ __device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf1
   l = (__bf16)(r1 - (float)m);
 }
 
+// split staging through split3_bf16x4: on in wg_x3_kernel (g_a.2 / g_s.4 wgrad
+// 1.28 -> 1.23 / 1.30 -> 1.27 ms), off in ig_kernel_x3s (1.14 -> 1.20 ms on
+// g_a.2 dgrad: the asm conversions constrain the MFMA interleave there)
+#ifndef IG_SPLIT_PK
+#define IG_SPLIT_PK 0
+#endif
+#ifndef WG_SPLIT_PK
+#define WG_SPLIT_PK 1
+#endif
+// split3_bf16 of four values with the bf16 conversions paired
+// (v_cvt_pk_bf16_f32 on two operands, round-to-nearest-even as the scalar
+// cast) and the residuals on v_pk_add_f32: 18 VALU per four values instead
+// of the 24 the compiler emits for four scalar splits.  Bitwise identical to
+// split3_bf16.  V4 is any 8-byte vector of four bf16.
+__device__ __forceinline__ uint32_t ic_cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+template <class V4>
+__device__ __forceinline__ void split3_bf16x4(floatx4v a, V4& h, V4& m, V4& l) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  u32x2 ph, pm, pl;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const f32x2 x = {a[2 * p], a[2 * p + 1]};
+    const uint32_t hh = ic_cvt_pk_bf16(x[0], x[1]);
+    const f32x2 r1 = x - f32x2{__uint_as_float(hh << 16), __uint_as_float(hh & 0xffff0000u)};
+    const uint32_t mm = ic_cvt_pk_bf16(r1[0], r1[1]);
+    const f32x2 r2 = r1 - f32x2{__uint_as_float(mm << 16), __uint_as_float(mm & 0xffff0000u)};
+    ph[p] = hh;
+    pm[p] = mm;
+    pl[p] = ic_cvt_pk_bf16(r2[0], r2[1]);
+  }
+  h = __builtin_bit_cast(V4, ph);
+  m = __builtin_bit_cast(V4, pm);
+  l = __builtin_bit_cast(V4, pl);
+}
+
 // 64-lane wave reduction (gfx950 wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -784,11 +784,15 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
         continue;
       }
       bf16x4 vh, vm, vl;
+      if (IG_SPLIT_PK) {
+        split3_bf16x4(sq ? ra[p] * ra[p] : ra[p], vh, vm, vl);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 h, m, l;
-        split3_bf16(sq ? ra[p][e] * ra[p][e] : ra[p][e], h, m, l);
-        vh[e] = h; vm[e] = m; vl[e] = l;
+        for (int e = 0; e < 4; ++e) {
+          __bf16 h, m, l;
+          split3_bf16(sq ? ra[p][e] * ra[p][e] : ra[p][e], h, m, l);
+          vh[e] = h; vm[e] = m; vl[e] = l;
+        }
       }
       __bf16* dst = &As[a_st + (NT / 8) * p * LDB];
       *(bf16x4*)dst = vh;

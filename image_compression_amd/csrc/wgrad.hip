@@ -529,15 +529,19 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
     for (int op = 0; op < 2; ++op) {
       const floatx4v v = op == 0 ? rg[q] : rx[q];
       wg_bf16x4 vh, vm, vl;
+      if (WG_SPLIT_PK && !(WG_X3_ABL & 2)) {
+        split3_bf16x4(v, vh, vm, vl);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 hh, mm, ll;
-        if (WG_X3_ABL & 2) {  // ablation: no split arithmetic
-          hh = mm = ll = (__bf16)v[e];
-        } else {
-          split3_bf16(v[e], hh, mm, ll);
+        for (int e = 0; e < 4; ++e) {
+          __bf16 hh, mm, ll;
+          if (WG_X3_ABL & 2) {  // ablation: no split arithmetic
+            hh = mm = ll = (__bf16)v[e];
+          } else {
+            split3_bf16(v[e], hh, mm, ll);
+          }
+          vh[e] = hh; vm[e] = mm; vl[e] = ll;
         }
-        vh[e] = hh; vm[e] = mm; vl[e] = ll;
       }
       __bf16* dst = base + op * OPER + srow[q] * PITCH + (scol[q] ^ (TWO ? ((srow[q] >> 1) & 1) << 5 : 0));
       *(wg_bf16x4*)dst = vh;
