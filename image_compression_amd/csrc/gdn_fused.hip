@@ -30,6 +30,9 @@
 // both operands.
 #include "../../include/imgcomp.h"
 #include "gemm.h"
+#ifndef GDN_SPLIT_PK
+#define GDN_SPLIT_PK 1  // split staging through split3_bf16x4 (paired conversions)
+#endif
 
 namespace {
 
@@ -269,11 +272,15 @@ __global__ void __launch_bounds__(768, 1)
       const int m = pos / (C / 4), lc = (pos - m * (C / 4)) ^ (m & 15);
       const floatx4v v = *(const floatx4v*)(xs + pos * 4);
       b4 vh, vm, vl;
+      if (GDN_SPLIT_PK) {
+        split3_bf16x4(v * v, vh, vm, vl);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 hh, mm, ll;
-        split3_bf16(v[e] * v[e], hh, mm, ll);
-        vh[e] = hh; vm[e] = mm; vl[e] = ll;
+        for (int e = 0; e < 4; ++e) {
+          __bf16 hh, mm, ll;
+          split3_bf16(v[e] * v[e], hh, mm, ll);
+          vh[e] = hh; vm[e] = mm; vl[e] = ll;
+        }
       }
       const int off = m * C + 8 * ((lc >> 1) ^ ((m >> 1) & 7)) + 4 * (lc & 1);
       *(b4*)(sq + off) = vh;
@@ -361,11 +368,15 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
 #pragma unroll
       for (int op = 0; op < 2; ++op) {
         b4 vh, vm, vl;
+        if (GDN_SPLIT_PK) {
+          split3_bf16x4(op == 0 ? qv : xv * xv, vh, vm, vl);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          __bf16 hh, mm, ll;
-          split3_bf16(op == 0 ? qv[e] : xv[e] * xv[e], hh, mm, ll);
-          vh[e] = hh; vm[e] = mm; vl[e] = ll;
+          for (int e = 0; e < 4; ++e) {
+            __bf16 hh, mm, ll;
+            split3_bf16(op == 0 ? qv[e] : xv[e] * xv[e], hh, mm, ll);
+            vh[e] = hh; vm[e] = mm; vl[e] = ll;
+          }
         }
         __bf16* dst = sb + op * 3 * PL + m * C + col;
         *(b4*)dst = vh;
