@@ -58,7 +58,7 @@ __device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf1
 
 // split staging through split3_bf16x4: on in wg_x3_kernel (g_a.2 / g_s.4 wgrad
 // 1.28 -> 1.23 / 1.30 -> 1.27 ms), off in ig_kernel_x3s (1.14 -> 1.20 ms on
-// g_a.2 dgrad: the asm conversions constrain the MFMA interleave there)
+// g_a.2 dgrad, with or without inline asm: fewer VALU, but a worse MFMA interleave)
 #ifndef IG_SPLIT_PK
 #define IG_SPLIT_PK 0
 #endif
@@ -71,9 +71,9 @@ __device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf1
 // of the 24 the compiler emits for four scalar splits.  Bitwise identical to
 // split3_bf16.  V4 is any 8-byte vector of four bf16.
 __device__ __forceinline__ uint32_t ic_cvt_pk_bf16(float lo, float hi) {
-  uint32_t r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));  // one v_cvt_pk_bf16_f32
 }
 template <class V4>
 __device__ __forceinline__ void split3_bf16x4(floatx4v a, V4& h, V4& m, V4& l) {
