@@ -57,10 +57,11 @@ __device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf1
 }
 
 // split staging through split3_bf16x4: on in wg_x3_kernel (g_a.2 / g_s.4 wgrad
-// 1.28 -> 1.23 / 1.30 -> 1.27 ms), off in ig_kernel_x3s (1.14 -> 1.20 ms on
-// g_a.2 dgrad, with or without inline asm: fewer VALU, but a worse MFMA interleave)
+// 1.28 -> 1.23 / 1.30 -> 1.27 ms) and in ig_kernel_x3s together with its
+// spread global loads (IG_X3_SGB = 8: big fwd/dgrad ops 5.30 -> 5.13 ms, with
+// the paired split 5.08; the paired split alone, loads up front, was slower)
 #ifndef IG_SPLIT_PK
-#define IG_SPLIT_PK 0
+#define IG_SPLIT_PK 1
 #endif
 #ifndef WG_SPLIT_PK
 #define WG_SPLIT_PK 1

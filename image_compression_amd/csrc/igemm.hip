@@ -14,6 +14,9 @@
 #ifndef IG_X3_REG
 #define IG_X3_REG 2  // split kernel: 2 swizzled register-staged (ig_kernel_x3s), 1 padded (ig_kernel_x3), 0 LDS-DMA (ig_kernel_x3d); 2 measured fastest
 #endif
+#ifndef IG_X3_SGB
+#define IG_X3_SGB 8  // ig_kernel_x3s: spread the next chunk's global loads, one per IG_X3_SGB MFMAs (0: compiler order, all loads up front)
+#endif
 #ifndef IG_X3S_ABL
 #define IG_X3S_ABL 0  // timing ablations of ig_kernel_x3s (results invalid): 1 no global loads, 4 no split/LDS store/barriers
 #endif
@@ -827,7 +830,10 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
     const __bf16* Ard = &As[(wm * WM + r) * LDB + ch];
     const __bf16* Brd = &Bs[(wn * WN + r) * LDB + ch];
     for (int c = cb; c < ce; ++c) {
-      if (c + 1 < ce) gload(c + 1);
+      // unconditional (the last chunk reloads itself, unused): the loads then share
+      // the MFMAs' basic block and can be spread among them (IG_X3_SGB)
+      if (IG_X3_SGB) gload(c + 1 < ce ? c + 1 : c);
+      else if (c + 1 < ce) gload(c + 1);
       bf16x8 a[NP][TM];
 #pragma unroll
       for (int q = 0; q < NP; ++q)
@@ -855,6 +861,14 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
       if (IG_X3S_ABL & 4) {  // ablation: no split / LDS store / barriers (keep the loads live)
         if (ra[0][0] == 12345.f) As[tid] = (__bf16)ra[0][1];
         continue;
+      }
+      if constexpr (IG_X3_SGB && NP == 3) {
+        // one global load per IG_X3_SGB MFMAs
+#pragma unroll
+        for (int k = 0; k < APASS + BPASS; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read
+          __builtin_amdgcn_sched_group_barrier(0x008, IG_X3_SGB, 0);  // MFMA
+        }
       }
       __syncthreads();
       if (c + 1 < ce) sstore();
