@@ -410,6 +410,9 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef WG_X3_ABL
 #define WG_X3_ABL 0  // timing ablations (results invalid): 1 no global loads, 2 no split, 4 no split/LDS stores, 8 no barrier
 #endif
+#ifndef WG_X3_SPREAD
+#define WG_X3_SPREAD 1  // row-fast refill loads issued per slot right after its store, spread among the MFMAs (4.40 -> 4.33 ms over all wgrad ops)
+#endif
 #ifndef WG_X3_DEPTH
 #define WG_X3_DEPTH 2  // steps of global loads in flight ahead of their split + store (2 or 3)
 #endif
@@ -459,6 +462,35 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
   // zero page: with the loads unconditional the compiler's vmcnt bookkeeping
   // keeps both register sets in flight (a branch around them made it drain all
   // loads, vmcnt(0), one step after they were issued)
+  // row-fast refill split per staged slot (WG_X3_SPREAD): the step's uniform
+  // bases once, then slot q's two loads right after slot q has been stored
+  struct RowBase {
+    const float* gb;
+    const float* xb;
+    int ix0;
+    bool rowok, live;
+  };
+  auto row_base = [&](uint32_t p0, bool live) {
+    const uint32_t img = fdiv(p0, d.fd_hw);
+    const uint32_t rr = p0 - img * d.fd_hw.d;
+    const uint32_t gy = fdiv(rr, d.fd_w);
+    const uint32_t gx0 = rr - gy * d.fd_w.d;
+    const int iy = (int)gy * d.stride + dyt;
+    return RowBase{d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w,
+                   d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h, (int)gx0 * d.stride + dxt,
+                   live && (unsigned)iy < (unsigned)d.Hx, live};
+  };
+  auto gload_q = [&](const RowBase& rb, int q, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    const int gcol = g0 + scol[q], xcol = c0 + scol[q];
+    const int ix = rb.ix0 + srow[q] * d.stride;
+    const float* gs = (rb.live && gcol < d.Cg) ? rb.gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
+    const float* xs = (rb.rowok && xcol < d.Cx && (unsigned)ix < (unsigned)d.Wx)
+                          ? rb.xb + (long long)ix * d.xs_w + xcol : wg_zero_page;
+    rg[q] = *(const floatx4v*)gs;
+    floatx4v vx = *(const floatx4v*)xs;
+    if (XSQ) vx = vx * vx;
+    rx[q] = vx;
+  };
   auto gload = [&](uint32_t p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP], bool live = true) {
     if (WG_X3_ABL & 1) {  // ablation: no global loads
 #pragma unroll
@@ -589,6 +621,10 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
         for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
     }
     static_assert(QP == TM, "one staged float4 per MFMA row group");
+    constexpr bool SPREAD = ROWFAST && !TWO && WG_X3_SPREAD && !(WG_X3_ABL & 1);
+    const uint32_t pn = (uint32_t)(p0 + (DEPTH + 1) * BK);
+    RowBase nb{};
+    if constexpr (SPREAD) nb = row_base(pn, (int)pn < (int)pe);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       wg_bf16x8 a[3];  // one row group's A fragments at a time (register pressure)
@@ -611,17 +647,19 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
       // the next step's split + store, one slice per MFMA row group, interleaved
       // with its MFMAs (unconditional: near the end it fills an unread buffer)
       sstore_q(buf ^ 1, i, rg, rx);
+      if constexpr (SPREAD) gload_q(nb, i, rg, rx);  // slot i refilled as soon as it is stored
       if constexpr (!TWO) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // MFMA
           __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // VALU
           __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+          if (SPREAD && (k == 2 || k == 5)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
         }
       }
     }
     // refill the set just stored: DEPTH steps ahead (never past the split: row-fast loads are unmasked)
-    if (ROWFAST || p0 + (DEPTH + 1) * BK < (int)pe)
+    if (!SPREAD && (ROWFAST || p0 + (DEPTH + 1) * BK < (int)pe))
       gload((uint32_t)(p0 + (DEPTH + 1) * BK), rg, rx, p0 + (DEPTH + 1) * BK < (int)pe);
     if (!(WG_X3_ABL & 8)) __syncthreads();
   };
