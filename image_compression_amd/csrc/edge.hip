@@ -55,25 +55,37 @@ struct EdgeGeom {
 // the global-load latency hides behind the current unit's MFMAs.
 constexpr int PREG = (PMAX + 255) / 256;
 
-__device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, long long u, float (&pr)[PREG], int tid) {
+// This thread's patch elements i = tid + 256 q, decomposed once per launch
+// (the divisions by the runtime patch width and kernel size are not redone
+// per unit): ky = -1 marks i >= C*k*PW.
+struct EdgePatchMap {
+  int ky[PREG], j[PREG], coff[PREG];
+};
+__device__ __forceinline__ void edge_patch_map(const EdgeGeom& g, EdgePatchMap& m, int tid) {
+  const int tot = g.C * g.k * g.PW;
+#pragma unroll
+  for (int q = 0; q < PREG; ++q) {
+    const int i = tid + 256 * q;
+    const int row = i / g.PW, j = i - (i / g.PW) * g.PW;
+    const int c = row / g.k, ky = row - (row / g.k) * g.k;
+    m.ky[q] = i < tot ? ky : -1;
+    m.j[q] = j;
+    m.coff[q] = i < tot ? (int)(c * g.sc) : 0;
+  }
+}
+__device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, const EdgePatchMap& m, long long u,
+                                                float (&pr)[PREG]) {
   const int seg = (int)(u % g.units_per_row);
   const long long r = u / g.units_per_row;
   const int oy = (int)(r % g.Ho);
   const int n = (int)(r / g.Ho);
   const int iy0 = oy * g.stride - g.pad, ix0 = seg * SEG * g.stride - g.pad;
-  const int tot = g.C * g.k * g.PW;
+  const float* xb = g.x + n * g.sn;
 #pragma unroll
   for (int q = 0; q < PREG; ++q) {
-    const int i = tid + 256 * q;
-    float v = 0.f;
-    if (i < tot) {
-      const int row = i / g.PW, j = i - (i / g.PW) * g.PW;
-      const int c = row / g.k, ky = row - (row / g.k) * g.k;
-      const int iy = iy0 + ky, ix = ix0 + j;
-      if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-        v = g.x[n * g.sn + c * g.sc + (long long)iy * g.sh + ix];
-    }
-    pr[q] = v;
+    const int iy = iy0 + m.ky[q], ix = ix0 + m.j[q];
+    const bool ok = m.ky[q] >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    pr[q] = ok ? xb[m.coff[q] + (long long)iy * g.sh + ix] : 0.f;
   }
 }
 
@@ -141,17 +153,19 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
     lds[bufsz + PSZ + i] = 0.f;
   }
 
+  EdgePatchMap pm;
+  edge_patch_map(g, pm, tid);
   long long u = blockIdx.x;
   int buf = 0;
   float pr[PREG];
   if (u < g.units) {
-    edge_patch_load(g, u, pr, tid);
+    edge_patch_load(g, pm, u, pr);
     edge_patch_store(g, pr, lds, tid);
   }
   for (; u < g.units; u += gridDim.x) {
     __syncthreads();  // patch `buf` complete; everyone is done with buf^1
     const long long un = u + gridDim.x;
-    if (un < g.units) edge_patch_load(g, un, pr, tid);
+    if (un < g.units) edge_patch_load(g, pm, un, pr);
     const float* patch = lds + buf * bufsz;
     floatx4v acc[SEG / 16][NTW];
 #pragma unroll
@@ -251,18 +265,20 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     }
   };
 
+  EdgePatchMap pm;
+  edge_patch_map(g, pm, tid);
   long long u = blockIdx.x;
   int buf = 0;
   float pr[PREG];
   if (u < g.units) {
     stage_g(u, lds);
-    edge_patch_load(g, u, pr, tid);
+    edge_patch_load(g, pm, u, pr);
     edge_patch_store(g, pr, pbase, tid);
   }
   for (; u < g.units; u += gridDim.x) {
     __syncthreads();  // vmcnt(0) + barrier: the G tile and patch `buf` are in LDS
     const long long un = u + gridDim.x;
-    if (un < g.units) edge_patch_load(g, un, pr, tid);
+    if (un < g.units) edge_patch_load(g, pm, un, pr);
     const float* gs = lds;
     const float* patch = pbase + buf * PB;
     // k-step s2 of the pixel reduction: pixel m = 4 s2 + lq
