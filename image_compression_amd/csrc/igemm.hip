@@ -17,6 +17,9 @@
 #ifndef IG_X3_SGB
 #define IG_X3_SGB 8  // ig_kernel_x3s: spread the next chunk's global loads, one per IG_X3_SGB MFMAs (0: compiler order, all loads up front)
 #endif
+#ifndef IG_BF16_SGB
+#define IG_BF16_SGB 2  // bf16 kernels: one next-chunk global load per IG_BF16_SGB MFMAs (0: loads up front; 2: C3 fwd/dgrad 2.59 -> 2.53 ms)
+#endif
 #ifndef IG_X3S_ABL
 #define IG_X3S_ABL 0  // timing ablations of ig_kernel_x3s (results invalid): 1 no global loads, 4 no split/LDS store/barriers
 #endif
@@ -417,7 +420,10 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
   const __bf16* Ard = &As[(wm * WM + r) * LDKB + 8 * h];
   const __bf16* Brd = &Bs[(wn * WN + r) * LDKB + 8 * h];
   for (int c = cb; c < ce; ++c) {
-    if (c + 1 < ce) gload(c + 1);
+    // unconditional with IG_BF16_SGB (the last chunk reloads itself, unused): the
+    // loads share the MFMAs' basic block and are spread among them
+    if (IG_BF16_SGB) gload(c + 1 < ce ? c + 1 : c);
+    else if (c + 1 < ce) gload(c + 1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8 a[TM], b[TN];
@@ -429,6 +435,13 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (IG_BF16_SGB > 0) {
+#pragma unroll
+      for (int k = 0; k < APASS + BPASS; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);            // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, IG_BF16_SGB, 0);  // MFMA
+      }
     }
     __syncthreads();
     if (c + 1 < ce) sstore();
@@ -862,12 +875,12 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
         if (ra[0][0] == 12345.f) As[tid] = (__bf16)ra[0][1];
         continue;
       }
-      if constexpr (IG_X3_SGB && NP == 3) {
-        // one global load per IG_X3_SGB MFMAs
+      if constexpr (IG_X3_SGB && (NP == 3 || IG_BF16_SGB)) {
+        // one global load per IG_X3_SGB MFMAs (bf16, NP = 1: per IG_BF16_SGB)
 #pragma unroll
         for (int k = 0; k < APASS + BPASS; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read
-          __builtin_amdgcn_sched_group_barrier(0x008, IG_X3_SGB, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? IG_X3_SGB : IG_BF16_SGB, 0);  // MFMA
         }
       }
       __syncthreads();
