@@ -39,12 +39,18 @@ class ICAdamWTensor(ctypes.Structure):
                 ("n", c_ll), ("lr", c_float), ("weight_decay", c_float)]
 
 
+class ICPlan(ctypes.Structure):
+    _fields_ = [("kernel", c_int), ("bm", c_int), ("bn", c_int), ("ksplit", c_int), ("nsplit", c_int),
+                ("im2col", c_int), ("variant", c_int), ("blocks", c_ll)]
+
+
 P = ctypes.POINTER
 _ACT = P(ICAct)
 
 # name -> (restype, argtypes); mirrors include/imgcomp.h one to one
 SIGNATURES = {
     "ic_version": (c_int, []),
+    "ic_conv_plan": (c_int, [c_int, _ACT, _ACT, c_int, c_int, c_int, c_int, P(ICPlan)]),
     "ic_device_sync_check": (c_int, [c_void]),
     "ic_conv2d_fwd_ws_ex": (c_size, [_ACT, c_int, c_int, c_int, _ACT, c_int]),
     "ic_conv2d_fwd_ex": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int, c_void, c_size,
@@ -99,6 +105,7 @@ SIGNATURES = {
     "ic_mse_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_void, c_void, c_void]),
     "ic_uniform": (c_int, [c_void, c_ll, c_ull, c_ull, c_void]),
     "ic_philox_advance": (c_int, [c_void, c_ull, c_void]),
+    "ic_philox_kat": (c_int, [c_void, c_void, c_int, c_void]),
     "ic_psnr": (c_int, [c_void, c_void, c_int, c_ll, c_float, c_void, c_void]),
     "ic_images_u8_to_input": (c_int, [c_void, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void, c_void, c_void,
                                       c_void]),
@@ -120,6 +127,22 @@ SIGNATURES = {
 
 _lib = None
 _load_error = None
+TORCH_OPS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libimgcomp_torch.so")
+_ops = None
+
+
+def ops():
+    """torch.ops.imgcomp (the TORCH_LIBRARY registration of the conv / GDN launchers,
+    csrc/torch_ops.cpp); loads libimgcomp_torch.so once, raises RuntimeError if absent."""
+    global _ops
+    if _ops is None:
+        load()
+        if not os.path.exists(TORCH_OPS_PATH):
+            raise RuntimeError(f"imgcomp: torch op library not built ({TORCH_OPS_PATH} missing); run "
+                               "`make -C image_compression_amd/csrc` or __graft_entry__.build()")
+        torch.ops.load_library(TORCH_OPS_PATH)
+        _ops = torch.ops.imgcomp
+    return _ops
 
 
 def load():
@@ -162,6 +185,29 @@ def act(t):
         raise RuntimeError(f"imgcomp: expected a 4-D tensor, got shape {tuple(t.shape)}")
     s = t.stride()
     return ICAct(c_void(t.data_ptr()), t.shape[0], t.shape[1], t.shape[2], t.shape[3], s[0], s[1], s[2], s[3])
+
+
+# ic_conv_plan op codes and kernel ids (include/imgcomp.h)
+OPS = {"conv2d_fwd": 0, "conv2d_dgrad": 1, "conv2d_wgrad": 2, "conv_transpose2d_fwd": 3,
+       "conv_transpose2d_dgrad": 4, "conv_transpose2d_wgrad": 5, "gdn_fwd": 6, "gdn_bwd": 7}
+KERNELS = {1: "ig_fp32", 2: "ig_fp32_gather", 3: "ig_bf16", 4: "ig_split", 5: "ig_split_bf16", 6: "edge_conv",
+           7: "im2col_gemm", 8: "tconv_few", 9: "tconv_few_rows", 10: "gemm_col2im", 11: "wg_fp32",
+           12: "wg_fp32_gather", 13: "wg_ldsdma", 14: "wg_split", 15: "edge_wgrad", 16: "gdn_fused",
+           17: "gdn_fused_split", 18: "gdn_gemm"}
+
+
+def plan(op, a, b=None, k=1, stride=1, pad=0, math=0):
+    """The launch plan (kernel, tile, K / pixel splits) that `op` takes for these operands
+    (ic_conv_plan; no launch).  a / b: tensors or ICAct, in the order of the op's
+    workspace query (fwd: x, y; dgrad: dy, dx; wgrad: x, dy; gdn: x)."""
+    L = load()
+    aa = a if isinstance(a, ICAct) else act(a)
+    bb = aa if b is None else (b if isinstance(b, ICAct) else act(b))
+    out = ICPlan()
+    rc = L.ic_conv_plan(OPS[op], aa, bb, k, stride, pad, int(math), ctypes.byref(out))
+    check(rc, f"plan({op})")
+    return {"kernel": KERNELS.get(out.kernel, out.kernel), "bm": out.bm, "bn": out.bn, "ksplit": out.ksplit,
+            "nsplit": out.nsplit, "im2col": out.im2col, "variant": out.variant, "blocks": out.blocks}
 
 
 def ptr(t):

@@ -128,21 +128,36 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* lds /* >= 16*NV
   __syncthreads();
 }
 
-// Philox4x32-10 counter-based RNG -> uniform float in [0,1) (24-bit mantissa)
-__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; the Random123 philox4x32_R with R = 10):
+// per round (hi, lo) = mulhilo(M0, c0), mulhilo(M1, c2); c = {hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0};
+// the key is bumped by the Weyl constants (0x9E3779B9, 0xBB67AE85) between rounds.
+// Pinned to the published Random123 known-answer vectors (tests/test_noise_gpu.py via ic_philox_kat;
+// oracle/philox.py restates it for the CPU tests).
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
-  uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
-  uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
-  c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
-}
-__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx) {
-  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), 0x9E3779B9u, 0x3C6EF372u};
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    philox_round(c, k0, k1);
+    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
-  return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+// The training-noise stream: element i of stream `seed` is word (i & 3) of
+// Philox4x32-10(counter {i >> 2 (64 bit), 0, 0}, key = seed), mapped to U[0,1)
+// by its top 24 bits.  Every Philox evaluation yields four consecutive
+// elements; streams are drawn from 4-aligned offsets (noise.py) so a thread
+// that handles elements 4j .. 4j+3 evaluates one block (philox_uniform4).
+__device__ __forceinline__ float philox_u24(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ floatx4v philox_uniform4(uint64_t seed, uint64_t blk) {
+  uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return floatx4v{philox_u24(c[0]), philox_u24(c[1]), philox_u24(c[2]), philox_u24(c[3])};
+}
+
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t idx) {
+  return philox_uniform4(seed, idx >> 2)[idx & 3];
 }

@@ -10,6 +10,8 @@
 #include "../../include/imgcomp.h"
 #include "gemm.h"
 
+thread_local ic_plan* g_plan_sink = nullptr;
+
 namespace {
 
 struct Carve {
@@ -42,7 +44,11 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
     // patch-gather kernel (edge.hip): no im2col columns in HBM
     const int Npad = ig_npad(y->c);
     const size_t wpb = (size_t)Npad * Kp * 4;
-    if (need) { *need = ic_align(wpb, 256); return IC_OK; }
+    if (need) {
+      plan_report(IC_KERNEL_EDGE_CONV, 64, y->c, 1, 0, 0, -1);
+      *need = ic_align(wpb, 256);
+      return IC_OK;
+    }
     if (wsb < wpb) return IC_ERR_WORKSPACE;
     float* wp = (float*)ws;
     int ky[IC_MAXT], kx[IC_MAXT];
@@ -69,7 +75,11 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
   const size_t xcb = (size_t)rows * Kp * 4;
   const size_t wpb = (size_t)d.Npad * Kp * 4;
   const size_t tot = ic_align(xcb, 256) + ic_align(wpb, 256) + ic_align(part, 256);
-  if (need) { *need = tot; return IC_OK; }
+  if (need) {
+    plan_report(IC_KERNEL_IM2COL_GEMM, d.bm, d.bn, d.ksplit, 0, 1, ig_grid_blocks(d));
+    *need = tot;
+    return IC_OK;
+  }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   float* xcol = cv.take(xcb);
@@ -113,7 +123,11 @@ int transposed_col2im(const ic_act* x, const float* W, const float* bias, int k,
   const size_t ycb = (size_t)rows * ncol * 4;
   const size_t wpb = (size_t)d.Npad * d.Kc * 4;
   const size_t tot = ic_align(ycb, 256) + ic_align(wpb, 256) + ic_align(part, 256);
-  if (need) { *need = tot; return IC_OK; }
+  if (need) {
+    plan_report(IC_KERNEL_GEMM_COL2IM, d.bm, d.bn, d.ksplit, 0, 1, ig_grid_blocks(d));
+    *need = tot;
+    return IC_OK;
+  }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   float* ycol = cv.take(ycb);
@@ -139,6 +153,7 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
                 int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
+  if (!act_fits32(x) || !act_fits32(y)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
   if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w)
     return IC_ERR_ARG;
   if (x->c <= FEW_CH && aop == AOP_NONE)
@@ -167,7 +182,11 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * esz;
   d.wplane = (long long)P.T * d.Npad * x->c;
   const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
-  if (need) { *need = tot; return IC_OK; }
+  if (need) {
+    plan_report(ig_kernel_kind(d), d.bm, d.bn, d.ksplit, 0, 0, ig_grid_blocks(d));
+    *need = tot;
+    return IC_OK;
+  }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   float* wp = cv.take(wpb);
@@ -183,12 +202,17 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
                     const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1 || stride > 2) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
+  if (!act_fits32(x) || !act_fits32(y)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
   if ((y->h + 2 * pad - k) / stride + 1 != x->h || (y->w + 2 * pad - k) / stride + 1 != x->w)
     return IC_ERR_ARG;
   if ((epi == EPI_NONE || epi == EPI_RELU) &&
       tconv_few_ok(x->c, y->c, k, stride, pad, x->sc, x->sw, x->sh, x->sn, x->h, x->w)) {
     // output-row-stationary kernel (edge.hip): no column buffer in HBM
-    if (need) { *need = 0; return IC_OK; }
+    if (need) {
+      plan_report(tconv_few_kind(x->h, x->w, k, pad, y->h), 0, y->c, 1, 0, 0, -1);
+      *need = 0;
+      return IC_OK;
+    }
     return tconv_few_run(x->data, x->n, x->h, x->w, x->c, W, y->c, k, pad, bias, epi == EPI_RELU, y->data, y->sn,
                          y->sc, y->sh, y->sw, y->h, y->w, s);
   }
@@ -238,7 +262,11 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
     d.wplane = (long long)ttot * d.Npad * x->c;
     const size_t wb = (size_t)d.wplane * 6;
     const size_t tot = ic_align(part, 256) + ic_align(wb, 256);
-    if (need) { *need = tot; return IC_OK; }
+    if (need) {
+      plan_report(ig_kernel_kind(d), d.bm, d.bn, d.ksplit, 0, 0, ig_grid_blocks(d));
+      *need = tot;
+      return IC_OK;
+    }
     if (wsb < tot) return IC_ERR_WORKSPACE;
     Carve cv{(char*)ws, 0};
     d.partial = part ? cv.take(part) : nullptr;
@@ -259,7 +287,11 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
     wpb[p] = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)d.ph[p].T * d.Npad * x->c * (d.bf16 ? 2 : 4);
     tot += ic_align(wpb[p], 256);
   }
-  if (need) { *need = tot; return IC_OK; }
+  if (need) {
+    plan_report(ig_kernel_kind(d), d.bm, d.bn, d.ksplit, 0, 0, ig_grid_blocks(d));
+    *need = tot;
+    return IC_OK;
+  }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   d.partial = part ? cv.take(part) : nullptr;
@@ -293,6 +325,7 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
                const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (G->n != X->n) return IC_ERR_ARG;
+  if (!act_fits32(G) || !act_fits32(X)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
   if ((X->h + 2 * pad - k) / stride + 1 != G->h || (X->w + 2 * pad - k) / stride + 1 != G->w)
     return IC_ERR_ARG;
   WgDesc d = {};
@@ -314,7 +347,11 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
     const int Kc = k * k * X->c + (db_from_g ? 1 : 0);
     const size_t slab = edge_wgrad_ws(G->c, Kc, edge_units(G->n, G->h, G->w));
     const size_t cs = (db && !db_from_g) ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
-    if (need) { *need = ic_align(slab, 256) + ic_align(cs, 256); return IC_OK; }
+    if (need) {
+      plan_report(IC_KERNEL_EDGE_WGRAD, G->c, Kc, 1, 0, 0, -1);
+      *need = ic_align(slab, 256) + ic_align(cs, 256);
+      return IC_OK;
+    }
     if (wsb < ic_align(slab, 256) + ic_align(cs, 256)) return IC_ERR_WORKSPACE;
     int rc = edge_wgrad_run(G->data, G->c, X->data, X->sn, X->sc, X->sh, X->sw, X->n, X->c, X->h, X->w, G->h, G->w,
                             k, stride, pad, dw, db_from_g ? db : nullptr, ws, s);
@@ -338,7 +375,15 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   const size_t part = wg_plan(d);
   const size_t cs = db ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
   const size_t tot = ic_align(part, 256) + ic_align(cs, 256) + ic_align(xcb, 256);
-  if (need) { *need = tot; return IC_OK; }
+  if (need) {
+    if (g_plan_sink) {
+      WgDesc q = d;
+      wg_prepare(q);
+      plan_report(wg_kernel_kind(q), q.bm, q.bn, 1, q.nsplit, few ? 1 : 0, wg_grid_blocks(q), q.rowfast);
+    }
+    *need = tot;
+    return IC_OK;
+  }
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   d.partial = cv.take(part);
@@ -376,7 +421,42 @@ size_t need_or_zero(int rc, size_t n) { return rc ? 0 : n; }
 
 extern "C" {
 
-int ic_version(void) { return 1; }
+int ic_version(void) { return 2; }
+
+int ic_conv_plan(int op, const ic_act* a, const ic_act* b, int k, int stride, int pad, int math, ic_plan* out) {
+  if (!out || !a || (!b && op != IC_OP_GDN_FWD && op != IC_OP_GDN_BWD)) return IC_ERR_ARG;
+  ic_plan p = {0, 0, 0, 1, 0, 0, 0, -1};
+  g_plan_sink = &p;
+  size_t n = 0;
+  int rc;
+  switch (op) {
+    case IC_OP_CONV2D_FWD:
+    case IC_OP_TCONV_DGRAD:
+      rc = direct_impl(a, nullptr, nullptr, k, stride, pad, b, EPI_NONE, AOP_NONE, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, 0, 0, &n, math);
+      break;
+    case IC_OP_CONV2D_DGRAD:
+    case IC_OP_TCONV_FWD:
+      rc = transposed_impl(a, nullptr, nullptr, k, stride, pad, b, EPI_NONE, nullptr, 0, 0, &n, math);
+      break;
+    case IC_OP_CONV2D_WGRAD:  // G = dy, X = x, bias from dy
+      rc = wgrad_impl(b, a, k, stride, pad, nullptr, b, (float*)1, nullptr, 0, 0, &n, math);
+      break;
+    case IC_OP_TCONV_WGRAD:   // G = x, X = dy, bias from dy
+      rc = wgrad_impl(a, b, k, stride, pad, nullptr, b, (float*)1, nullptr, 0, 0, &n, math);
+      break;
+    case IC_OP_GDN_FWD:
+    case IC_OP_GDN_BWD:
+      rc = gdn_plan(op == IC_OP_GDN_BWD, a, math);
+      break;
+    default:
+      rc = IC_ERR_ARG;
+  }
+  g_plan_sink = nullptr;
+  if (rc == IC_OK && p.kernel == 0) rc = IC_ERR_ARG;
+  if (rc == IC_OK) *out = p;
+  return rc;
+}
 
 size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math) {
   size_t n = 0;

@@ -711,6 +711,11 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
   return IC_OK;
 }
 
+int tconv_few_kind(int Hin, int Win, int k, int pad, int Hout) {
+  return (TCONV_FEW2 && Win <= 128 && k <= 5 && (Hout - 1 + pad) / 2 <= Hin + 2) ? IC_KERNEL_TCONV_FEW_ROWS
+                                                                                 : IC_KERNEL_TCONV_FEW;
+}
+
 // transposed conv 2x upsampling of a wide NHWC map to <= 4 channels (see tconv_few_kernel)
 bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, long long xsw, long long xsh,
                   long long xsn, int Hin, int Win) {
@@ -723,7 +728,7 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
                   const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
                   int Hout, int Wout, hipStream_t s) {
   if (((uintptr_t)x & 15) || Hout < 1 || Wout < 1) return IC_ERR_ARG;
-  if (TCONV_FEW2 && Win <= 128 && k <= 5 && (Hout - 1 + pad) / 2 <= Hin + 2) {
+  if (tconv_few_kind(Hin, Win, k, pad, Hout) == IC_KERNEL_TCONV_FEW_ROWS) {
     // input-row stationary: runs of input rows, about one block per CU
     long long run = ((long long)N * Hin + 255) / 256;
     if (run < 4) run = 4;

@@ -165,15 +165,33 @@ __global__ void sqdiff_bwd_k(const float* a, const float* b, const float* g, lon
   }
 }
 
+// u[i] = element off + i of the stream (off % 4 == 0): one Philox block per thread and quad
 __global__ void uniform_k(float* u, long long n, unsigned long long seed, unsigned long long off) {
-  GRID_STRIDE(i, n) u[i] = philox_uniform(seed, off + (unsigned long long)i);
+  const long long nq = (n + 3) >> 2;
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq; j += (long long)gridDim.x * blockDim.x) {
+    const floatx4v r = philox_uniform4(seed, (off >> 2) + (unsigned long long)j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (4 * j + e < n) u[4 * j + e] = r[e];
+  }
+}
+
+// raw Philox4x32-10 blocks for the known-answer test: in[6 i ..] = {c0, c1, c2, c3, k0, k1}
+__global__ void philox_kat_k(const uint32_t* in, uint32_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t c[4] = {in[6 * i], in[6 * i + 1], in[6 * i + 2], in[6 * i + 3]};
+  philox4x32_10(c, in[6 * i + 4], in[6 * i + 5]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[4 * i + e] = c[e];
 }
 
 }  // namespace
 
 namespace {
+// the stream base moves in whole Philox blocks (multiples of 4 elements)
 __global__ void philox_advance_k(unsigned long long* state, unsigned long long n) {
-  if (threadIdx.x == 0) state[1] += n;
+  if (threadIdx.x == 0) state[1] += (n + 3) & ~3ull;
 }
 }  // namespace
 
@@ -265,7 +283,16 @@ int ic_sqdiff_bwd(const float* a, const float* b, const float* g, long long n, f
   return IC_OK;
 }
 int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset, void* stream) {
-  hipLaunchKernelGGL(uniform_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, u, n, seed, offset);
+  if (offset & 3) return IC_ERR_ARG;
+  if (n <= 0) return IC_OK;
+  hipLaunchKernelGGL(uniform_k, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, u, n, seed, offset);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_philox_kat(const unsigned* in, unsigned* out, int n, void* stream) {
+  if (n <= 0) return IC_OK;
+  hipLaunchKernelGGL(philox_kat_k, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, out, n);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }

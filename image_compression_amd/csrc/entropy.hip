@@ -234,15 +234,34 @@ __device__ __forceinline__ float dcdf_gauss(float v) {
   return 0.5f * TWO_OVER_SQRTPI * expf(-t * t) * RSQRT2;
 }
 
+__device__ __forceinline__ void cond_elem(const float* y, const float* sc, const float* mean, long long i, int kind,
+                                          float uu, int mode, float* qo, float* po) {
+  const float qv = mode == 1 ? rintf(y[i]) : y[i] + (uu - 0.5f);
+  qo[i] = qv;
+  const float a = fabsf(qv - (mean ? mean[i] : 0.f));
+  const float s = sc[i];
+  const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
+  po[i] = kind == 0 ? cdf_lap(vu) - cdf_lap(vl) : cdf_gauss(vu) - cdf_gauss(vl);
+}
+
+// one quad of elements per thread and iteration: in the Philox modes one Philox block
+// (four uniforms) serves the quad (stream offsets are 4-aligned)
 __global__ void cond_fwd_k(const float* y, const float* sc, const float* mean, long long n, int kind, int mode,
                            const float* u, unsigned long long seed, unsigned long long off, float* qo, float* po) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float qv = quant(y[i], mode, u, i, seed, off);
-    qo[i] = qv;
-    const float a = fabsf(qv - (mean ? mean[i] : 0.f));
-    const float s = sc[i];
-    const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
-    po[i] = kind == 0 ? cdf_lap(vu) - cdf_lap(vl) : cdf_gauss(vu) - cdf_gauss(vl);
+  const long long nq = (n + 3) >> 2;
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq; j += (long long)gridDim.x * blockDim.x) {
+    floatx4v r = {0.f, 0.f, 0.f, 0.f};
+    if (mode == 3) {
+      const unsigned long long* st = (const unsigned long long*)u;
+      r = philox_uniform4(st[0], ((st[1] + off) >> 2) + (unsigned long long)j);
+    } else if (mode == 2) {
+      r = philox_uniform4(seed, (off >> 2) + (unsigned long long)j);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * j + e;
+      if (i < n) cond_elem(y, sc, mean, i, kind, mode == 0 ? u[i] : r[e], mode, qo, po);
+    }
   }
 }
 
@@ -291,7 +310,8 @@ int ic_conditional_fwd(const float* y, const float* scale, const float* mean, lo
                        const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
                        void* stream) {
   if (mode == 0 && !u) return IC_ERR_ARG;
-  long long b = (n + 255) / 256;
+  if (mode == 2 && (offset & 3)) return IC_ERR_ARG;  // stream offsets are whole Philox blocks
+  long long b = (n + 1023) / 1024;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
   hipLaunchKernelGGL(cond_fwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, y, scale, mean, n, kind,

@@ -165,6 +165,33 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
 
 }  // namespace
 
+// ic_conv_plan(IC_OP_GDN_*): the dispatch conditions of gdn_fwd_impl / gdn_bwd_impl
+int gdn_plan(int bwd, const ic_act* x, int math) {
+  if (!act_fits32(x)) return IC_ERR_ARG;
+  const long long P = (long long)x->n * x->h * x->w;
+  const bool fused = gdn_fused_ok(x->data, x->data, x->data, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P);
+  const bool split = (math & IC_MATH_SPLIT) != 0;
+  if (!bwd) {
+    const bool fsplit = split && x->c % 32 == 0 && x->sc == 1 && x->c >= 64;
+    if ((!fsplit || x->c == 192) && fused) {
+      plan_report(fsplit ? IC_KERNEL_GDN_FUSED_SPLIT : IC_KERNEL_GDN_FUSED, fsplit ? 32 : 16, x->c, 1, 0, 0, -1);
+      return IC_OK;
+    }
+  } else if (fused) {
+    plan_report(split && x->c == 192 ? IC_KERNEL_GDN_FUSED_SPLIT : IC_KERNEL_GDN_FUSED, 16, x->c, 1, 0, 0, -1);
+    return IC_OK;
+  }
+  size_t n = 0;
+  ic_plan* sink = g_plan_sink;
+  g_plan_sink = nullptr;
+  const int rc = bwd ? gdn_bwd_impl(x, nullptr, nullptr, nullptr, 0, x, nullptr, nullptr, nullptr, 0, 0, &n, math)
+                     : gdn_fwd_impl(x, nullptr, nullptr, 0, x, nullptr, nullptr, 0, 0, &n, math);
+  g_plan_sink = sink;
+  if (rc) return rc;
+  plan_report(IC_KERNEL_GDN_GEMM, 0, x->c, 1, 0, 0, -1);
+  return IC_OK;
+}
+
 extern "C" {
 
 size_t ic_gdn_fwd_ws(const ic_act* x) {

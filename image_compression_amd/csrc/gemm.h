@@ -11,6 +11,7 @@
 //        dW[g][(t,c)] = sum_p G[p][g] * X[p*s + d_t][c]
 #pragma once
 #include "common.h"
+#include "../../include/imgcomp.h"
 
 enum IgEpilogue {
   EPI_NONE = 0,
@@ -63,6 +64,9 @@ struct IgDesc {
 // Fill tile choice, mtiles, split-K; returns partial-buffer bytes needed.
 size_t ig_plan(IgDesc& d);
 int ig_run(IgDesc& d, hipStream_t s);
+// IC_KERNEL_* that ig_run launches for a planned descriptor, and its grid size
+int ig_kernel_kind(const IgDesc& d);
+long long ig_grid_blocks(const IgDesc& d);
 // N padding the packed-weight layout must use for `Cout`
 int ig_npad(int Cout);
 
@@ -91,6 +95,31 @@ struct WgDesc {
 
 size_t wg_plan(WgDesc& d);
 int wg_run(WgDesc& d, hipStream_t s);
+// launch-time fields (fast divisors, row-fast mode); then the IC_KERNEL_* wg_run launches and its grid
+void wg_prepare(WgDesc& d);
+int wg_kernel_kind(const WgDesc& d);
+long long wg_grid_blocks(const WgDesc& d);
+
+// launch-plan reporting (ic_conv_plan): set for the calling thread by the query entry point; the
+// ops' workspace-query paths fill it when it is non-null
+extern thread_local ic_plan* g_plan_sink;
+static inline void plan_report(int kernel, int bm, int bn, int ksplit, int nsplit, int im2col, long long blocks,
+                               int variant = 0) {
+  if (!g_plan_sink) return;
+  g_plan_sink->kernel = kernel; g_plan_sink->bm = bm; g_plan_sink->bn = bn; g_plan_sink->ksplit = ksplit;
+  g_plan_sink->nsplit = nsplit; g_plan_sink->im2col = im2col; g_plan_sink->blocks = blocks;
+  g_plan_sink->variant = variant;
+}
+// element offsets the kernels index with 32-bit arithmetic: every addressed element of `a` below 2^31
+static inline bool act_fits32(const ic_act* a) {
+  if (a->n < 0 || a->c < 0 || a->h < 0 || a->w < 0) return false;
+  long long mx = 0;
+  const long long ext[4] = {a->n, a->c, a->h, a->w}, st[4] = {a->sn, a->sc, a->sh, a->sw};
+  for (int i = 0; i < 4; ++i) {
+    if (ext[i] > 1) mx += (ext[i] - 1) * (st[i] < 0 ? -st[i] : st[i]);
+  }
+  return mx < (1LL << 31) && (long long)a->n * a->h * a->w < (1LL << 31);
+}
 // out[g][c][kk(t)] (+)= sum over splits; kk_of_t maps tap -> ky*k+kx, kk = k*k
 int wg_reduce(const WgDesc& d, float* out, const int* kk_of_t, int kk, hipStream_t s);
 
@@ -140,6 +169,10 @@ bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, 
 int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float* W, int Cout, int k, int pad,
                   const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
                   int Hout, int Wout, hipStream_t s);
+// IC_KERNEL_TCONV_FEW_ROWS or IC_KERNEL_TCONV_FEW: which one tconv_few_run launches
+int tconv_few_kind(int Hin, int Win, int k, int pad, int Hout);
+// ic_conv_plan for GDN (gdn.hip): reports through g_plan_sink
+int gdn_plan(int bwd, const ic_act* x, int math);
 size_t edge_wgrad_ws(int CG, int Kc, long long units);
 int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
                    int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,

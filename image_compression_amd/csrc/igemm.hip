@@ -11,38 +11,17 @@
 // per chunk are contiguous in LDS -> 4 x ds_read_b128 per operand tile.
 #include "gemm.h"
 
-#ifndef IG_X3_REG
-#define IG_X3_REG 2  // split kernel: 2 swizzled register-staged (ig_kernel_x3s), 1 padded (ig_kernel_x3), 0 LDS-DMA (ig_kernel_x3d); 2 measured fastest
-#endif
 #ifndef IG_X3_SGB
 #define IG_X3_SGB 8  // ig_kernel_x3s: spread the next chunk's global loads, one per IG_X3_SGB MFMAs (0: compiler order, all loads up front)
 #endif
 #ifndef IG_BF16_SGB
 #define IG_BF16_SGB 2  // bf16 kernels: one next-chunk global load per IG_BF16_SGB MFMAs (0: loads up front; 2: C3 fwd/dgrad 2.59 -> 2.53 ms)
 #endif
-#ifndef IG_X3S_ABL
-#define IG_X3S_ABL 0  // timing ablations of ig_kernel_x3s (results invalid): 1 no global loads, 4 no split/LDS store/barriers
-#endif
 #ifndef IG_BF16_S
 // bf16 operands on small maps (64-row tiles) on ig_kernel_x3s's swizzled 16x16x32
 // structure, one product: 0.056 vs 0.072-0.080 ms on g_a.6 / g_s.0 (the padded
 // 64-channel-chunk kernel keeps the 128-row tiles: 0.378 vs 0.412 ms on g_a.2)
 #define IG_BF16_S 1
-#endif
-#ifndef IG_X3_M16
-#define IG_X3_M16 true  // ig_kernel_x3s on v_mfma_f32_16x16x32_bf16 (7-8 % faster than 32x32x16 on the conv fwd layers: DVFS holds a higher clock)
-#endif
-#ifndef IG_X3_BM256
-#define IG_X3_BM256 0  // > 0: 256-row 8-wave split tiles for maps with at least this many output pixels
-#endif
-#ifndef IG_X3_BM64
-#define IG_X3_BM64 0  // 1: 64-row tiles (3 blocks per CU) for every split-kernel layer
-#endif
-#ifndef IG_X3_NST
-#define IG_X3_NST 3  // LDS stages of the LDS-DMA split kernel
-#endif
-#ifndef IG_X3_ABL
-#define IG_X3_ABL 0  // ablation builds (tools/abl_build.sh): 1 no weight reloads, 2 no activation reloads, 3 no MFMA
 #endif
 
 namespace {
@@ -454,174 +433,18 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
 // The fp32 implicit GEMM on the bf16 MFMA: every fp32 operand is split exactly
 // into three bf16 terms (split3_bf16), and the six cross products that carry
 // the product down to 2^-24 of its size are accumulated in fp32 on
-// v_mfma_f32_32x32x16_bf16 (1/16 the cycles of the fp32 MFMA per product, so
-// six of them cost 3/8 of v_mfma_f32_32x32x2_f32's time per MAC).  The error
-// is that of an fp32 fma chain (tests/test_ops_gpu.py pins it against the
-// fp64 oracle beside the native fp32 kernel).  Activations are read as fp32
-// and split on their way into LDS; weights arrive as three pre-split bf16
-// planes.  K chunk = 32 channels of one tap (Cin % 32 == 0), channel-chunk
-// outer / tap inner as in ig_kernel; LDS rows of 40 bf16 (80 B) keep the
-// 16-B fragment reads of 16 consecutive rows on distinct banks.
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256, 2) ig_kernel_x3(const IgDesc d) {
-  constexpr int LDB = 40;
-  constexpr int WAVES_N = BN / WN;
-  constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int APASS = BM / 32, BPASS = BN / 64;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(BN % 64 == 0, "B staged 64 rows per pass");
-  __shared__ __attribute__((aligned(16))) __bf16 As[3 * BM * LDB];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * BN * LDB];
-
-  const int zi = blockIdx.z;
-  const int phase = zi / d.ksplit;
-  const int split = zi - phase * d.ksplit;
-  const IgPhase& P = d.ph[phase];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  const int n0 = blockIdx.y * BN;
-  const int nchunks = P.T * (d.Cin >> 5);
-  const int cb = split * d.kcps;
-  const int ce = min(nchunks, cb + d.kcps);
-
-  const int tid = threadIdx.x;
-  const int lrow = tid >> 3, lc4 = tid & 7;   // A: 8 float4 per 32-channel row
-  const int brow = tid >> 2, bq = tid & 3;    // B: 4 x 16 B per 32-wide bf16 row
-  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
-  uint32_t a_off[APASS];
-  int a_iy[APASS], a_ix[APASS];
-#pragma unroll
-  for (int p = 0; p < APASS; ++p) {
-    const uint32_t m = m0 + lrow + 32 * p;
-    const bool ok = m < M;
-    const uint32_t mm = ok ? m : 0u;
-    const uint32_t img = fdiv(mm, P.fd_hw);
-    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
-    const uint32_t gy = fdiv(rem, P.fd_w);
-    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
-    a_iy[p] = ok ? (int)gy * d.stride : -0x40000000;
-    a_ix[p] = (int)gx * d.stride;
-    a_off[p] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[p] * xsh + (uint32_t)a_ix[p] * xsw;
-  }
-  const float* __restrict__ xg = d.x;
-  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-  const size_t wplane = (size_t)d.wplane;
-
-  floatx4v ra[APASS];
-  bf16x8 rb[3][BPASS];
-  auto gload = [&](int c) {
-    const int cc = c / P.T, t = c - cc * P.T;
-    const int dy = P.dy[t], dx = P.dx[t];
-    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
-#if IG_X3_ABL == 2
-    if (c == cb)
-#endif
-#pragma unroll
-    for (int p = 0; p < APASS; ++p) {
-      const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
-      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
-      const float* src = in ? xg + (a_off[p] + toff) : ig_zero_page;
-      ra[p] = *(const floatx4v*)src;
-    }
-    const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 32 + bq * 8;
-#if IG_X3_ABL == 1
-    if (c == cb)
-#endif
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int p = 0; p < BPASS; ++p) rb[q][p] = *(const bf16x8*)(wb + q * wplane + (size_t)(64 * p) * d.Cin);
-  };
-  auto sstore = [&]() {
-#pragma unroll
-    for (int p = 0; p < APASS; ++p) {
-      bf16x4 vh, vm, vl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 h, m, l;
-        split3_bf16(ra[p][e], h, m, l);
-        vh[e] = h; vm[e] = m; vl[e] = l;
-      }
-      __bf16* dst = &As[(lrow + 32 * p) * LDB + lc4 * 4];
-      *(bf16x4*)dst = vh;
-      *(bf16x4*)(dst + BM * LDB) = vm;
-      *(bf16x4*)(dst + 2 * BM * LDB) = vl;
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[(q * BN + brow + 64 * p) * LDB + bq * 8] = rb[q][p];
-  };
-
-  const int lane = tid & 63, w = tid >> 6;
-  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
-  const int r = lane & 31, h = lane >> 5;
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  if (cb < ce) {
-    gload(cb);
-    sstore();
-  }
-  __syncthreads();
-  const __bf16* Ard = &As[(wm * WM + r) * LDB + 8 * h];
-  const __bf16* Brd = &Bs[(wn * WN + r) * LDB + 8 * h];
-  for (int c = cb; c < ce; ++c) {
-    if (c + 1 < ce) gload(c + 1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 a[3][TM], b[3][TN];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 32) * LDB + 16 * s);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(Brd + (q * BN + j * 32) * LDB + 16 * s);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-#if IG_X3_ABL == 3
-          if (acc[i][j][0] == 12345.f) acc[i][j] += (floatx16)(float)(a[0][i][0] + a[1][i][1] + a[2][i][2] + b[0][j][0] + b[1][j][1] + b[2][j][2]);
-          continue;
-#endif
-          // small terms first, the leading product last
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
-        }
-    }
-    __syncthreads();
-    if (c + 1 < ce) sstore();
-    __syncthreads();
-  }
-  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
-}
-
-
-// ------------------------------------------------------------------ split, swizzled, MFMA shape choice
-// ig_kernel_x3 with unpadded 64-B LDS rows (32 bf16 of one K chunk) whose four
-// 16-B chunks are XOR-swizzled by row: chunk c of row r sits at
-// c ^ ig_swz(r), ig_swz(r) = (0, 2, 3, 1)[(r >> 2) & 3], which keeps the
-// ds_read_b128 fragment reads of both MFMA shapes on distinct banks in every
-// 16-lane group (and the 8/16-lane write groups on distinct dword banks):
-// 60 KB of LDS per block instead of 77.  M16 selects v_mfma_f32_16x16x32_bf16
-// (16x16 tiles, K 32 per instruction: lane (r16, g) holds 8 k of chunk g)
-// instead of v_mfma_f32_32x32x16_bf16 (lane (r, h) holds chunk 2s + h of K
-// step s): the same cycles per MAC, but the chip may hold a different clock.
+// v_mfma_f32_16x16x32_bf16 (1/16 the cycles of the fp32 MFMA per product, so
+// six of them cost 3/8 of v_mfma_f32_32x32x2_f32's time per MAC).
+// Activations are read as fp32 and split on their way into LDS; weights
+// arrive as three pre-split bf16 planes.  K chunk = 32 channels of one tap
+// (Cin % 32 == 0), channel-chunk outer / tap inner as in ig_kernel.
+// LDS rows are 64 B (32 bf16 of one K chunk) whose four 16-B chunks are
+// XOR-swizzled by row: chunk c of row r sits at c ^ ig_swz(r),
+// ig_swz(r) = (0, 2, 3, 1)[(r >> 2) & 3], which keeps the ds_read_b128
+// fragment reads (lane (r16, g) holds 8 k of chunk g) on distinct banks in
+// every 16-lane group, and the 8/16-lane write groups on distinct dword banks.
+// The 16x16x32 shape runs 7-8 % faster than 32x32x16 at equal cycles per MAC:
+// the chip holds a higher clock (MI355X_MICROARCH.md, DVFS item 7).
 __device__ __forceinline__ int ig_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
 template <int TM, int TN>
@@ -688,14 +511,12 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
     }
 }
 
-// NT = 64 x (BM/WM) x (BN/WN) threads: 4 waves (128-row tiles, two blocks per
-// CU) or 8 waves (256-row tiles, one block per CU: each weight chunk staged
-// once per 256 output pixels)
-// NP = 3: the exact split (six products); NP = 1: plain bf16 operands (RN of
-// the activations, bf16-packed weights) with fp32 accumulation, one product
-template <int BM, int BN, int WM, int WN, bool M16, int NP = 3>
+// NT = 64 x (BM/WM) x (BN/WN) = 256 threads: 4 waves, two blocks per CU (three
+// for 64-row tiles).  NP = 3: the exact split (six products); NP = 1: plain
+// bf16 operands (RN of the activations, bf16-packed weights) with fp32
+// accumulation, one product (C3 on maps <= 32^2)
+template <int BM, int BN, int WM, int WN, int NP = 3>
 __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)) ig_kernel_x3s(const IgDesc d) {
-  static_assert(NP == 3 || (NP == 1 && M16), "bf16 mode on the 16x16x32 MFMA only");
   constexpr int LDB = 32;
   constexpr int WAVES_N = BN / WN;
   constexpr int NT = 64 * (BM / WM) * (BN / WN);
@@ -763,13 +584,6 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   floatx4v ra[APASS];
   bf16x8 rb[BPASS];
   auto gload = [&](int c) {
-    if (IG_X3S_ABL & 1) {  // ablation: no global loads
-#pragma unroll
-      for (int p = 0; p < APASS; ++p) ra[p] = floatx4v{(float)c, 1.f, 2.f, 3.f};
-#pragma unroll
-      for (int p = 0; p < BPASS; ++p) rb[p] = bf16x8{};
-      return;
-    }
     const int cc = c / P.T, t = c - cc * P.T;
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32 + lc4 * 4);
@@ -826,301 +640,63 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   const int lane = tid & 63, w = tid >> 6;
   const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
 
-  if constexpr (M16) {
-    constexpr int TM = WM / 16, TN = WN / 16;
-    const int r = lane & 15, g = lane >> 4;
-    floatx4v acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    if (cb < ce) {
-      gload(cb);
-      sstore();
-    }
-    __syncthreads();
-    const int ch = 8 * (g ^ ig_swz(r));
-    const __bf16* Ard = &As[(wm * WM + r) * LDB + ch];
-    const __bf16* Brd = &Bs[(wn * WN + r) * LDB + ch];
-    for (int c = cb; c < ce; ++c) {
-      // unconditional (the last chunk reloads itself, unused): the loads then share
-      // the MFMAs' basic block and can be spread among them (IG_X3_SGB)
-      if (IG_X3_SGB) gload(c + 1 < ce ? c + 1 : c);
-      else if (c + 1 < ce) gload(c + 1);
-      bf16x8 a[NP][TM];
-#pragma unroll
-      for (int q = 0; q < NP; ++q)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 16) * LDB);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        bf16x8 b[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if constexpr (NP == 1) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
-            continue;
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
-        }
-      }
-      if (IG_X3S_ABL & 4) {  // ablation: no split / LDS store / barriers (keep the loads live)
-        if (ra[0][0] == 12345.f) As[tid] = (__bf16)ra[0][1];
-        continue;
-      }
-      if constexpr (IG_X3_SGB && (NP == 3 || IG_BF16_SGB)) {
-        // one global load per IG_X3_SGB MFMAs (bf16, NP = 1: per IG_BF16_SGB)
-#pragma unroll
-        for (int k = 0; k < APASS + BPASS; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read
-          __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? IG_X3_SGB : IG_BF16_SGB, 0);  // MFMA
-        }
-      }
-      __syncthreads();
-      if (c + 1 < ce) sstore();
-      __syncthreads();
-    }
-    ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
-  } else {
-    constexpr int TM = WM / 32, TN = WN / 32;
-    const int r = lane & 31, h = lane >> 5;
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    if (cb < ce) {
-      gload(cb);
-      sstore();
-    }
-    __syncthreads();
-    const int sw = ig_swz(r);
-    const __bf16* Ard = &As[(wm * WM + r) * LDB];
-    const __bf16* Brd = &Bs[(wn * WN + r) * LDB];
-    for (int c = cb; c < ce; ++c) {
-      if (c + 1 < ce) gload(c + 1);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int ch = 8 * ((2 * s2 + h) ^ sw);
-        bf16x8 a[3][TM], b[3][TN];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 32) * LDB + ch);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(Brd + (q * BN + j * 32) * LDB + ch);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
-          }
-      }
-      __syncthreads();
-      if (c + 1 < ce) sstore();
-      __syncthreads();
-    }
-    ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
-  }
-}
-
-// ------------------------------------------------------------------ split, LDS-DMA staged
-// Same arithmetic as ig_kernel_x3, staged without a VGPR round trip: each
-// 16-channel K chunk (one tap) arrives by LDS-DMA (global_load_lds_dwordx4)
-// into an NST-deep ring of LDS stages, chunk c + NST - 1 in flight while chunk
-// c computes, one barrier per chunk.  The activations land as fp32 and are
-// split into their three bf16 terms in registers as the A fragments are read;
-// the weights land as the three pre-split bf16 planes.  LDS-DMA writes its
-// 64 lanes' 16-B pieces lane-linearly, so the bank swizzles are applied on the
-// DMA source side:
-//   A stage [BM rows][4 x 16-B chunks of fp32]: chunk c of row r at c ^ ((r >> 2) & 3)
-//   B plane [BN rows][2 x 16-B chunks of bf16]: chunk c of row n at c ^ ((n >> 3) & 1)
-// which keeps every 16-lane group of the ds_read_b128 fragment reads on
-// distinct banks (MI355X_MICROARCH.md §LDS lane groups).
-typedef __attribute__((address_space(3))) void* ig_lds_t;
-typedef const __attribute__((address_space(1))) void* ig_gbl_t;
-
-// DMA instructions wave w issues per stage, and a counted wait that leaves
-// the later stages' DMAs in flight
-constexpr int ig_cntw(int ins, int pw, int w) {
-  int n = 0;
-  for (int j = 0; j < pw; ++j) n += (4 * j + w < ins) ? 1 : 0;
-  return n;
-}
-template <int N>
-__device__ __forceinline__ void ig_vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-}
-
-template <int BM, int BN, int WM, int WN, int NST>
-__global__ void __launch_bounds__(256, 2) ig_kernel_x3d(const IgDesc d) {
-  constexpr int WAVES_N = BN / WN;
-  constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_BYTES = BM * 64;
-  constexpr int B_PLANE = BN * 32;
-  constexpr int STAGE = A_BYTES + 3 * B_PLANE;
-  constexpr int A_INS = A_BYTES / 1024, B_INS = 3 * B_PLANE / 1024;  // 1-KB wave DMA instructions per stage
-  constexpr int A_PW = (A_INS + 3) / 4, B_PW = (B_INS + 3) / 4;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "whole DMA instructions");
-  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
-
-  const int zi = blockIdx.z;
-  const int phase = zi / d.ksplit;
-  const int split = zi - phase * d.ksplit;
-  const IgPhase& P = d.ph[phase];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  const int n0 = blockIdx.y * BN;
-  const int nchunks = P.T * (d.Cin >> 4);
-  const int cb = split * d.kcps;
-  const int ce = min(nchunks, cb + d.kcps);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
-  const float* __restrict__ xg = d.x;
-  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-
-  // per DMA instruction j of this wave: the row (pixel) it feeds and its channel offset
-  uint32_t a_off[A_PW];
-  int a_iy[A_PW], a_ix[A_PW];
-#pragma unroll
-  for (int j = 0; j < A_PW; ++j) {
-    const int g = j * 4 + w;
-    const int o = g * 1024 + lane * 16;
-    const int r = o >> 6, cp = (o >> 4) & 3;
-    const int c = cp ^ ((r >> 2) & 3);
-    const uint32_t m = m0 + r;
-    const bool ok = g < A_INS && m < M;
-    const uint32_t mm = ok ? m : 0u;
-    const uint32_t img = fdiv(mm, P.fd_hw);
-    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
-    const uint32_t gy = fdiv(rem, P.fd_w);
-    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
-    a_iy[j] = ok ? (int)gy * d.stride : -0x40000000;
-    a_ix[j] = (int)gx * d.stride;
-    a_off[j] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[j] * xsh + (uint32_t)a_ix[j] * xsw + (uint32_t)(c * 4);
-  }
-  uint32_t b_off[B_PW];
-#pragma unroll
-  for (int j = 0; j < B_PW; ++j) {
-    const int g = j * 4 + w;
-    const int o = g * 1024 + lane * 16;
-    const int q = o / B_PLANE, rem = o - q * B_PLANE;
-    const int n = rem >> 5, cp = (rem >> 4) & 1;
-    const int c = cp ^ ((n >> 3) & 1);
-    b_off[j] = (uint32_t)(q * d.wplane) + (uint32_t)(n0 + n) * (uint32_t)d.Cin + (uint32_t)(c * 8);
-  }
-  const uint32_t tstride = (uint32_t)d.Npad * (uint32_t)d.Cin;
-
-  auto stage = [&](int c, int buf) {
-    const int cc = c / P.T, t = c - cc * P.T;
-    const int dy = P.dy[t], dx = P.dx[t];
-    char* base = lds + buf * STAGE;
-    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 16);
-#pragma unroll
-    for (int j = 0; j < A_PW; ++j) {
-      if (j * 4 + w < A_INS) {  // wave-uniform
-        const int iy = a_iy[j] + dy, ix = a_ix[j] + dx;
-        const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
-        const float* src = in ? xg + (a_off[j] + toff) : ig_zero_page;
-        __builtin_amdgcn_global_load_lds((ig_gbl_t)src, (ig_lds_t)(base + (j * 4 + w) * 1024), 16, 0, 0);
-      }
-    }
-    const uint32_t woff = (uint32_t)t * tstride + (uint32_t)(cc * 16);
-#pragma unroll
-    for (int j = 0; j < B_PW; ++j) {
-      if (j * 4 + w < B_INS)
-        __builtin_amdgcn_global_load_lds((ig_gbl_t)(wpb + (b_off[j] + woff)),
-                                         (ig_lds_t)(base + A_BYTES + (j * 4 + w) * 1024), 16, 0, 0);
-    }
-  };
-
-  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
-  const int r = lane & 31, h = lane >> 5;
-  floatx16 acc[TM][TN];
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int r = lane & 15, g = lane >> 4;
+  floatx4v acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // fragment byte offsets inside a stage (row bits above 4 do not change the swizzles)
-  const int sa = (r >> 2) & 3;
-  const int a_rd0 = (wm * WM + r) * 64 + 16 * ((2 * h) ^ sa);
-  const int a_rd1 = (wm * WM + r) * 64 + 16 * ((2 * h + 1) ^ sa);
-  const int b_rd = A_BYTES + (wn * WN + r) * 32 + 16 * (h ^ ((r >> 3) & 1));
-
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (cb + s < ce) stage(cb + s, s);
-  int buf = 0;
-  for (int c = cb; c < ce; ++c) {
-    // own DMAs of chunk c have landed (those of the NST-2 later chunks may still fly), then barrier
-    if (NST > 2 && c + 1 < ce) {
-      switch (w) {
-        case 0: ig_vm_wait<ig_cntw(A_INS, A_PW, 0) + ig_cntw(B_INS, B_PW, 0)>(); break;
-        case 1: ig_vm_wait<ig_cntw(A_INS, A_PW, 1) + ig_cntw(B_INS, B_PW, 1)>(); break;
-        case 2: ig_vm_wait<ig_cntw(A_INS, A_PW, 2) + ig_cntw(B_INS, B_PW, 2)>(); break;
-        default: ig_vm_wait<ig_cntw(A_INS, A_PW, 3) + ig_cntw(B_INS, B_PW, 3)>(); break;
-      }
-    } else {
-      ig_vm_wait<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (c + NST - 1 < ce) stage(c + NST - 1, (buf + NST - 1) % NST);
-    const char* sb = lds + buf * STAGE;
-    bf16x8 a[3][TM], b[3][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const floatx4v v0 = *(const floatx4v*)(sb + a_rd0 + i * 32 * 64);
-      const floatx4v v1 = *(const floatx4v*)(sb + a_rd1 + i * 32 * 64);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        __bf16 hh, mm, ll;
-        split3_bf16(e < 4 ? v0[e] : v1[e - 4], hh, mm, ll);
-        a[0][i][e] = hh; a[1][i][e] = mm; a[2][i][e] = ll;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[q][j] = *(const bf16x8*)(sb + b_rd + q * B_PLANE + j * 32 * 32);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
-      }
-    buf = buf + 1 == NST ? 0 : buf + 1;
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  if (cb < ce) {
+    gload(cb);
+    sstore();
   }
-  ig_epilogue<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, r, h, split);
+  __syncthreads();
+  const int ch = 8 * (g ^ ig_swz(r));
+  const __bf16* Ard = &As[(wm * WM + r) * LDB + ch];
+  const __bf16* Brd = &Bs[(wn * WN + r) * LDB + ch];
+  for (int c = cb; c < ce; ++c) {
+    // unconditional (the last chunk reloads itself, unused): the loads then share
+    // the MFMAs' basic block and can be spread among them (IG_X3_SGB)
+    if (IG_X3_SGB) gload(c + 1 < ce ? c + 1 : c);
+    else if (c + 1 < ce) gload(c + 1);
+    bf16x8 a[NP][TM];
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[q][i] = *(const bf16x8*)(Ard + (q * BM + i * 16) * LDB);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (NP == 1) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+          continue;
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+      }
+    }
+    if constexpr (IG_X3_SGB && (NP == 3 || IG_BF16_SGB)) {
+      // one global load per IG_X3_SGB MFMAs (bf16, NP = 1: per IG_BF16_SGB)
+#pragma unroll
+      for (int k = 0; k < APASS + BPASS; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? IG_X3_SGB : IG_BF16_SGB, 0);  // MFMA
+      }
+    }
+    __syncthreads();
+    if (c + 1 < ce) sstore();
+    __syncthreads();
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
 }
 
 // split-K reduction + epilogue: one thread per (row, channel)
@@ -1158,42 +734,34 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
   dim3 grid(mt, d.Npad / BN, d.nphase * d.ksplit);
   const bool sq = d.a_op == AOP_SQUARE;
-  if constexpr ((BM / WM) * (BN / WN) == 8) {  // 8-wave tiles: split kernel only
-    if (!d.x3) return IC_ERR_ARG;
-    hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, IG_X3_M16>), grid, dim3(512), 0, s, d);
-    IC_CHECK_LAUNCH();
-    return IC_OK;
-  } else if (d.bf16) {
-    if (sq) return IC_ERR_ARG;
-    if constexpr (BN % 64 == 0 && BM == 64) {
-      if (IG_BF16_S) {
-        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, true, 1>), grid, dim3(256), 0, s, d);
-        IC_CHECK_LAUNCH();
-        return IC_OK;
+  switch (ig_kernel_kind(d)) {
+    case IC_KERNEL_IG_SPLIT_BF16:
+      if constexpr (BN % 64 == 0 && BM == 64) {
+        if (sq) return IC_ERR_ARG;
+        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, d);
+        break;
       }
-    }
-    if (BM == 64) return IC_ERR_ARG;
-    hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
-  } else if (d.x3) {
-    if constexpr (BN % 64 == 0) {
-#if IG_X3_REG == 2
-      hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, IG_X3_M16>), grid, dim3(256), 0, s, d);
-#elif IG_X3_REG
-      if (sq) return IC_ERR_ARG;
-      hipLaunchKernelGGL((ig_kernel_x3<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
-#else
-      if (sq) return IC_ERR_ARG;
-      hipLaunchKernelGGL((ig_kernel_x3d<BM, BN, WM, WN, IG_X3_NST>), grid, dim3(256), 0, s, d);
-#endif
-    } else {
       return IC_ERR_ARG;
-    }
-  } else if (d.generic) {
-    if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
-  } else {
-    if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, d);
+    case IC_KERNEL_IG_BF16:
+      if constexpr (BM != 64) {
+        if (sq) return IC_ERR_ARG;
+        hipLaunchKernelGGL((ig_kernel_bf16<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+        break;
+      }
+      return IC_ERR_ARG;
+    case IC_KERNEL_IG_SPLIT:
+      if constexpr (BN % 64 == 0) {
+        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+        break;
+      }
+      return IC_ERR_ARG;
+    case IC_KERNEL_IG_FP32_GATHER:
+      if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, s, d);
+      else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
+      break;
+    default:
+      if (sq) hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, d);
+      else hipLaunchKernelGGL((ig_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, d);
   }
   IC_CHECK_LAUNCH();
   return IC_OK;
@@ -1221,9 +789,7 @@ size_t ig_plan(IgDesc& d) {
   if (d.Cout % 192 == 0) {
     // small maps (hyperprior and <= 32x32 at batch 32): 64-row tiles double the tile
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
-    d.bm = ((!d.bf16 || IG_BF16_S) && (mall < 65536 || (IG_X3_BM64 && d.x3))) ? 64 : 128;
-    // split kernel on large maps: 256-row, 8-wave tiles (weights staged once per 256 pixels)
-    if (IG_X3_BM256 && d.x3 && IG_X3_REG == 2 && mall >= IG_X3_BM256) d.bm = 256;
+    d.bm = ((!d.bf16 || IG_BF16_S) && mall < 65536) ? 64 : 128;
     d.bn = 192;
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
@@ -1243,7 +809,7 @@ size_t ig_plan(IgDesc& d) {
     mtot += M;
     tiles += (long long)P.mtiles * (d.Npad / d.bn);
     const int nch = d.generic ? (d.Kc >> 5)
-                  : P.T * (ig_bf16_wide(d) ? (d.Cin >> 6) : (d.x3 && IG_X3_REG == 0) ? (d.Cin >> 4) : (d.Cin >> 5));
+                  : P.T * (ig_bf16_wide(d) ? (d.Cin >> 6) : (d.Cin >> 5));
     nchunks_max = nch > nchunks_max ? nch : nchunks_max;
   }
   d.Mtot = mtot;
@@ -1266,6 +832,18 @@ size_t ig_plan(IgDesc& d) {
   return (size_t)d.ksplit * (size_t)mtot * (size_t)d.Cout * sizeof(float);
 }
 
+int ig_kernel_kind(const IgDesc& d) {
+  if (d.bf16) return ig_bf16_wide(d) ? IC_KERNEL_IG_BF16 : IC_KERNEL_IG_SPLIT_BF16;
+  if (d.x3) return IC_KERNEL_IG_SPLIT;
+  return d.generic ? IC_KERNEL_IG_FP32_GATHER : IC_KERNEL_IG_FP32;
+}
+
+long long ig_grid_blocks(const IgDesc& d) {
+  int mt = 0;
+  for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
+  return (long long)mt * (d.Npad / d.bn) * d.nphase * d.ksplit;
+}
+
 int ig_run(IgDesc& d, hipStream_t s) {
   if (d.Mtot == 0) return IC_OK;
   if (!d.generic && (d.Cin % 32 != 0 || d.xs_c != 1)) return IC_ERR_ARG;
@@ -1273,8 +851,7 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
-  if (d.bn == 192 && d.bm == 256) rc = ig_launch_t<256, 192, 64, 96>(d, s);
-  else if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
+  if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
   else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);
   else rc = ig_launch_t<256, 32, 64, 32>(d, s);

@@ -13,9 +13,6 @@
 // per operand fragment (ds_read_b32, conflict-free).
 #include "gemm.h"
 
-#ifndef WG_X3_PAIR
-#define WG_X3_PAIR 0  // 1: one 8-wave block per CU over two taps (wg_x3p_kernel; measured 19 % slower)
-#endif
 #ifndef WG_X3_TWO
 #define WG_X3_TWO 0  // split wgrad: 1 = two blocks per CU (swizzled unpadded rows), 0 = one (padded rows)
 #endif
@@ -407,9 +404,6 @@ typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 // TWO: two blocks per CU — unpadded 192-bf16 rows whose 16-B chunks are
 // XOR-swizzled by 4 on rows with bit 1 set (the four rows of a transposed read
 // then start 0 / 32 / 16 / 48 dwords apart mod 64), 74 KB of LDS per block.
-#ifndef WG_X3_ABL
-#define WG_X3_ABL 0  // timing ablations (results invalid): 1 no global loads, 2 no split, 4 no split/LDS stores, 8 no barrier
-#endif
 #ifndef WG_X3_SPREAD
 #define WG_X3_SPREAD 1  // row-fast refill loads issued per slot right after its store, spread among the MFMAs (4.40 -> 4.33 ms over all wgrad ops)
 #endif
@@ -492,14 +486,6 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
     rx[q] = vx;
   };
   auto gload = [&](uint32_t p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP], bool live = true) {
-    if (WG_X3_ABL & 1) {  // ablation: no global loads
-#pragma unroll
-      for (int q = 0; q < QP; ++q) {
-        rg[q] = floatx4v{(float)p0, 1.f, 2.f, 3.f};
-        rx[q] = floatx4v{(float)(p0 + q), 1.f, 2.f, 3.f};
-      }
-      return;
-    }
     if (ROWFAST) {
       // a 16-pixel step never crosses an output row: image / row / first column are uniform
       const uint32_t img = fdiv(p0, d.fd_hw);
@@ -552,26 +538,18 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
   // split + store one staged float4 of each operand (q), so the store pass can
   // be spread between the MFMA groups of the previous step
   auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
-    if (WG_X3_ABL & 4) {  // ablation: no split, no LDS stores (keep the loads live)
-      if (rg[q][0] == 12345.f && rx[q][1] == 54321.f) lds[tid] = (__bf16)rg[q][2];
-      return;
-    }
     __bf16* base = lds + buf * STAGE;
 #pragma unroll
     for (int op = 0; op < 2; ++op) {
       const floatx4v v = op == 0 ? rg[q] : rx[q];
       wg_bf16x4 vh, vm, vl;
-      if (WG_SPLIT_PK && !(WG_X3_ABL & 2)) {
+      if (WG_SPLIT_PK) {
         split3_bf16x4(v, vh, vm, vl);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           __bf16 hh, mm, ll;
-          if (WG_X3_ABL & 2) {  // ablation: no split arithmetic
-            hh = mm = ll = (__bf16)v[e];
-          } else {
-            split3_bf16(v[e], hh, mm, ll);
-          }
+          split3_bf16(v[e], hh, mm, ll);
           vh[e] = hh; vm[e] = mm; vl[e] = ll;
         }
       }
@@ -621,7 +599,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
         for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE + tr_row + ((wn * WN + j * 32 + tr_col) ^ tr_sw));
     }
     static_assert(QP == TM, "one staged float4 per MFMA row group");
-    constexpr bool SPREAD = ROWFAST && !TWO && WG_X3_SPREAD && !(WG_X3_ABL & 1);
+    constexpr bool SPREAD = ROWFAST && !TWO && WG_X3_SPREAD;
     const uint32_t pn = (uint32_t)(p0 + (DEPTH + 1) * BK);
     RowBase nb{};
     if constexpr (SPREAD) nb = row_base(pn, (int)pn < (int)pe);
@@ -661,7 +639,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
     // refill the set just stored: DEPTH steps ahead (never past the split: row-fast loads are unmasked)
     if (!SPREAD && (ROWFAST || p0 + (DEPTH + 1) * BK < (int)pe))
       gload((uint32_t)(p0 + (DEPTH + 1) * BK), rg, rx, p0 + (DEPTH + 1) * BK < (int)pe);
-    if (!(WG_X3_ABL & 8)) __syncthreads();
+    __syncthreads();
   };
 
   // steps run in pairs (with DEPTH 2 the two register sets alternate
@@ -731,194 +709,6 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 }
 
 
-// Tap-pair variant: one block of 8 waves per CU computes the weight gradient
-// of TWO taps over the same pixel range — waves 0-3 tap 2tp, waves 4-7 tap
-// 2tp+1, each as the 4-wave kernel above (96x96 wave tiles, 144 AGPR-free
-// accumulators).  The G operand (the same for every tap) is staged once per
-// step for both; two waves per SIMD hide each other's barrier and read
-// latency.  LDS per buffer: G (3 planes) + X of both taps (6 planes), 448-B
-// rows; two buffers (129 KB).
-template <bool ROWFAST, bool XSQ>
-__global__ void __launch_bounds__(512) wg_x3p_kernel(const WgDesc d) {
-  constexpr int BM = 192, BN = 192, WM = 96, WN = 96, BK = 16;
-  constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int PITCH = 224;
-  constexpr int PLANE = BK * PITCH;
-  constexpr int OPER = 3 * PLANE;
-  constexpr int STAGE = 3 * OPER;           // G, X(tap 0), X(tap 1)
-  constexpr int C4 = BM / 4;                // float4 per staged row
-  constexpr int NSLOT = 3 * BK * C4;        // float4 slots per step (G + 2 X)
-  constexpr int QP = (NSLOT + 511) / 512;   // 5
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
-
-  const int tiles = d.mtiles * d.ntiles;
-  const int TP = (d.T + 1) >> 1;            // tap pairs
-  const int nblk = tiles * TP * d.nsplit;
-  const int b = blockIdx.x;
-  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
-  if (wid >= nblk) return;
-  const int per_split = tiles * TP;
-  const int split = wid / per_split;
-  const int bx = wid - split * per_split;
-  const int tp = bx / tiles;
-  const int rem = bx - tp * tiles;
-  const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
-  const int g0 = mt * BM, c0 = nt * BN;
-  const uint32_t pb = (uint32_t)split * (uint32_t)d.pps;
-  uint32_t pe = pb + (uint32_t)d.pps;
-  if (pe > (uint32_t)d.P) pe = (uint32_t)d.P;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int t0 = 2 * tp, t1 = 2 * tp + 1;
-  const bool has1 = t1 < d.T;
-  const int dy0 = d.dy[t0], dx0 = d.dx[t0];
-  const int dy1 = has1 ? d.dy[t1] : 0, dx1 = has1 ? d.dx[t1] : 0;
-
-  // staging slots: s < BK*C4 -> G; then X of tap 0, X of tap 1
-  int sop[QP], srow[QP], scol[QP];
-  bool sok[QP];
-#pragma unroll
-  for (int q = 0; q < QP; ++q) {
-    const int f = tid + 512 * q;
-    sok[q] = f < NSLOT && (f < 2 * BK * C4 || has1);
-    const int op = f / (BK * C4), g = f - op * (BK * C4);
-    sop[q] = op;
-    srow[q] = g / C4;
-    scol[q] = (g - (g / C4) * C4) * 4;
-  }
-  floatx4v rs[QP];
-  auto gload = [&](uint32_t p0) {
-    uint32_t img = 0, gy = 0, gx0 = 0;
-    if (ROWFAST) {
-      img = fdiv(p0, d.fd_hw);
-      const uint32_t rr = p0 - img * d.fd_hw.d;
-      gy = fdiv(rr, d.fd_w);
-      gx0 = rr - gy * d.fd_w.d;
-    }
-#pragma unroll
-    for (int q = 0; q < QP; ++q) {
-      const float* src = wg_zero_page;
-      uint32_t im = img, yy = gy, xx = gx0 + srow[q];
-      bool pin = true;
-      if (!ROWFAST) {
-        const uint32_t p = p0 + srow[q];
-        pin = p < pe;
-        const uint32_t pp = pin ? p : 0u;
-        im = fdiv(pp, d.fd_hw);
-        const uint32_t rr = pp - im * d.fd_hw.d;
-        yy = fdiv(rr, d.fd_w);
-        xx = rr - yy * d.fd_w.d;
-      }
-      if (sok[q] && pin) {
-        if (sop[q] == 0) {
-          const int gcol = g0 + scol[q];
-          if (gcol < d.Cg) src = d.g + (long long)im * d.gs_n + (long long)yy * d.gs_h + (long long)xx * d.gs_w + gcol;
-        } else {
-          const int xcol = c0 + scol[q];
-          const int iy = (int)yy * d.stride + (sop[q] == 1 ? dy0 : dy1);
-          const int ix = (int)xx * d.stride + (sop[q] == 1 ? dx0 : dx1);
-          if (xcol < d.Cx && (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)
-            src = d.x + (long long)im * d.xs_n + (long long)iy * d.xs_h + (long long)ix * d.xs_w + xcol;
-        }
-      }
-      floatx4v v = *(const floatx4v*)src;
-      if (XSQ && sop[q] != 0) v = v * v;
-      rs[q] = v;
-    }
-  };
-  auto sstore_q = [&](int buf, int q) {
-    if (!sok[q]) return;
-    __bf16* base = lds + buf * STAGE + sop[q] * OPER + srow[q] * PITCH + scol[q];
-    wg_bf16x4 vh, vm, vl;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      __bf16 hh, mm, ll;
-      split3_bf16(rs[q][e], hh, mm, ll);
-      vh[e] = hh; vm[e] = mm; vl[e] = ll;
-    }
-    *(wg_bf16x4*)base = vh;
-    *(wg_bf16x4*)(base + PLANE) = vm;
-    *(wg_bf16x4*)(base + 2 * PLANE) = vl;
-  };
-
-  const int ts = w >> 2, wq = w & 3, wm = wq >> 1, wn = wq & 1;
-  const int r = lane & 31, h = lane >> 5;
-  const int li = lane & 15;
-  const int tr_row = (8 * h + (li >> 2)) * PITCH;
-  const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  auto tr8 = [&](const __bf16* src) {
-    const wg_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)src);
-    const wg_bf16x4 hi =
-        __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) wg_bf16x4*)(src + 4 * PITCH));
-    return (wg_bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  const bool active = ts == 0 || has1;  // wave-uniform
-
-  if (pb < pe) {
-    gload(pb);
-#pragma unroll
-    for (int q = 0; q < QP; ++q) sstore_q(0, q);
-    if (pb + BK < pe) gload(pb + BK);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (uint32_t p0 = pb; p0 < pe; p0 += BK) {
-    const __bf16* sb = lds + buf * STAGE;
-    const __bf16* xb = sb + (1 + ts) * OPER;
-    const bool more = p0 + BK < pe;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (active) {
-        wg_bf16x8 a[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE + tr_row + wm * WM + i * 32 + tr_col);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          wg_bf16x8 bq[3];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) bq[q] = tr8(xb + q * PLANE + tr_row + wn * WN + j * 32 + tr_col);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bq[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[0], acc[i][j], 0, 0, 0);
-        }
-      }
-      // the next step's split + store behind this row group's MFMAs (slots 2i, 2i+1)
-      if (more) {
-        if (2 * i < QP) sstore_q(buf ^ 1, 2 * i);
-        if (2 * i + 1 < QP) sstore_q(buf ^ 1, 2 * i + 1);
-      }
-    }
-    if (more && p0 + 2 * BK < pe) gload(p0 + 2 * BK);
-    __syncthreads();
-    buf ^= 1;
-  }
-  static_assert(2 * TM >= QP, "every staged slot is stored behind some row group");
-
-  if (!active) return;
-  const int t = ts ? t1 : t0;
-  float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int gr = g0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (gr >= d.Cg) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = c0 + wn * WN + j * 32 + r;
-        if (col < d.ncols) slab[(long long)gr * d.ncols + col] = acc[i][j][reg];
-      }
-    }
-}
 
 struct WgRed {
   const float* partial;
@@ -997,18 +787,6 @@ int wg_glds_launch_t(const WgDesc& d, hipStream_t s) {
 
 int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   const bool sq = d.x_op == AOP_SQUARE;
-  if (WG_X3_PAIR) {
-    dim3 gp((d.mtiles * d.ntiles * ((d.T + 1) / 2) * d.nsplit + 7) / 8 * 8);
-    if (d.rowfast) {
-      if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true, true>), gp, dim3(512), 0, s, d);
-      else hipLaunchKernelGGL((wg_x3p_kernel<true, false>), gp, dim3(512), 0, s, d);
-    } else {
-      if (sq) hipLaunchKernelGGL((wg_x3p_kernel<false, true>), gp, dim3(512), 0, s, d);
-      else hipLaunchKernelGGL((wg_x3p_kernel<false, false>), gp, dim3(512), 0, s, d);
-    }
-    IC_CHECK_LAUNCH();
-    return IC_OK;
-  }
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
   if (d.rowfast) {
@@ -1139,7 +917,7 @@ size_t wg_plan(WgDesc& d) {
   d.ntiles = ic_cdiv(d.ncols, d.bn);
   d.P = (long long)d.N * d.Hg * d.Wg;
   const long long tiles = (long long)d.mtiles * d.ntiles *
-                          (d.generic ? 1 : ((d.x3 && WG_X3_PAIR) ? (d.T + 1) / 2 : d.T));
+                          (d.generic ? 1 : d.T);
   // one full wave of blocks: 256 CUs x 2 resident blocks = 512 slots, so a
   // grid of just over 512 equal blocks would run at half speed; never fewer
   // than 64 pixels per split
@@ -1160,30 +938,47 @@ size_t wg_plan(WgDesc& d) {
   return ic_align(slab, 256) + lvl2;
 }
 
-int wg_run(WgDesc& d, hipStream_t s) {
-  if (d.P == 0) return IC_OK;
-  if (d.P >= (1LL << 31)) return IC_ERR_ARG;  // 32-bit pixel indexing
+void wg_prepare(WgDesc& d) {
   d.fd_hw = make_fastdiv((uint32_t)((long long)d.Hg * d.Wg));
   d.rowfast = d.Wg % 16 == 0 && d.pps % 16 == 0 && d.gs_w * 16 < (1LL << 31) &&
               (long long)d.stride * 16 * d.xs_w < (1LL << 31);
   d.fd_w = make_fastdiv((uint32_t)d.Wg);
   d.g_vec = (d.gs_c == 1 && d.Cg % 4 == 0);
+}
+
+int wg_kernel_kind(const WgDesc& d) {
   // LDS-DMA path: 16-B aligned float4 rows in both operands
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   const bool glds_ok = d.g_vec && !d.generic && a16(d.g) && a16(d.x) && d.gs_w % 4 == 0 && d.gs_h % 4 == 0 &&
                        d.gs_n % 4 == 0 && d.xs_w % 4 == 0 && d.xs_h % 4 == 0 && d.xs_n % 4 == 0;
+  if (d.generic) return IC_KERNEL_WG_FP32_GATHER;
+  if (d.x3) return IC_KERNEL_WG_SPLIT;
+  return glds_ok ? IC_KERNEL_WG_LDSDMA : IC_KERNEL_WG_FP32;
+}
+
+int wg_run(WgDesc& d, hipStream_t s) {
+  if (d.P == 0) return IC_OK;
+  if (d.P >= (1LL << 31)) return IC_ERR_ARG;  // 32-bit pixel indexing
+  wg_prepare(d);
   if (!d.generic && (d.xs_c != 1 || d.Cx % 4 != 0)) return IC_ERR_ARG;
-  if (d.generic) return wg_launch_t<192, 64, 96, 32, true>(d, s);
-  if (d.x3) {
-    if (!d.g_vec || d.bn != 192 || d.bm != 192) return IC_ERR_ARG;
-    return wg_x3_launch(d, s);
+  switch (wg_kernel_kind(d)) {
+    case IC_KERNEL_WG_FP32_GATHER:
+      return wg_launch_t<192, 64, 96, 32, true>(d, s);
+    case IC_KERNEL_WG_SPLIT:
+      if (!d.g_vec || d.bn != 192 || d.bm != 192) return IC_ERR_ARG;
+      return wg_x3_launch(d, s);
+    case IC_KERNEL_WG_LDSDMA:
+      if (d.bn == 192) return wg_glds_launch_t<192, 192, 96, 96>(d, s);
+      return wg_glds_launch_t<192, 64, 96, 32>(d, s);
+    default:
+      if (d.bn == 192) return wg_launch_t<192, 192, 96, 96, false>(d, s);
+      return wg_launch_t<192, 64, 96, 32, false>(d, s);
   }
-  if (glds_ok) {
-    if (d.bn == 192) return wg_glds_launch_t<192, 192, 96, 96>(d, s);
-    return wg_glds_launch_t<192, 64, 96, 32>(d, s);
-  }
-  if (d.bn == 192) return wg_launch_t<192, 192, 96, 96, false>(d, s);
-  return wg_launch_t<192, 64, 96, 32, false>(d, s);
+}
+
+long long wg_grid_blocks(const WgDesc& d) {
+  if (d.generic) return (d.mtiles * d.ntiles * d.nsplit + 7) / 8 * 8;
+  return ((long long)d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8;
 }
 
 int wg_reduce(const WgDesc& d, float* out, const int* kk_of_t, int kk, hipStream_t s) {

@@ -74,116 +74,100 @@ def _n(t):
     return ctypes.c_longlong(t.numel())
 
 
+# launch-plan log (tests): while a list is installed by `record_plans`, every conv / GDN op
+# appends the plan (ic_conv_plan) of each launch it makes, so a test can show which kernel
+# instances a whole training step ran
+_PLAN_LOG = None
+
+
+class record_plans:
+    def __enter__(self):
+        global _PLAN_LOG
+        self.log, _PLAN_LOG = [], []
+        return _PLAN_LOG
+
+    def __exit__(self, *exc):
+        global _PLAN_LOG
+        _PLAN_LOG = None
+        return False
+
+
+def _log_plan(op, a, b, k=1, stride=1, pad=0, math=0):
+    if _PLAN_LOG is not None:
+        _PLAN_LOG.append(dict(_lib.plan(op, a, b, k, stride, pad, math), op=op))
+
+
 # ============================================================== convolutions
 class Conv2dFn(Function):
-    """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56)."""
+    """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56), each
+    launch one torch.ops.imgcomp op (csrc/torch_ops.cpp -> C ABI)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, act, math=0):
         _lib.require_device(x, weight, bias)
-        L = _L()
         x = _cl(x)
         w = weight.contiguous()
         b = None if bias is None else bias.contiguous()
-        N, Cin, H, W = x.shape
-        Cout, Cin_w, k, k2 = w.shape
-        if Cin_w != Cin or k != k2:
+        if w.shape[1] != x.shape[1] or w.shape[2] != w.shape[3]:
             raise RuntimeError(f"conv2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
-        Ho = (H + 2 * padding - k) // stride + 1
-        Wo = (W + 2 * padding - k) // stride + 1
-        y = _new_act(N, Cout, Ho, Wo, x.device)
-        ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_conv2d_fwd_ws_ex(ax, k, stride, padding, ay, int(math))
-        buf = _ws(nb, x.device)
-        _lib.check(L.ic_conv2d_fwd_ex(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act), int(math),
-                                      _lib.ptr(buf), nb, _lib.stream_of(x)), "conv2d_fwd")
-        ctx.conf = (stride, padding, k, act, b is not None, int(math))
+        y = _lib.ops().conv2d_fwd(x, w, b, stride, padding, int(act), int(math))
+        _log_plan("conv2d_fwd", x, y, w.shape[2], stride, padding, math)
+        ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, padding, k, act, has_b, math = ctx.conf
-        L = _L()
+        stride, padding, act, has_b, math = ctx.conf
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
         dx = dw = db = None
-        st = _lib.stream_of(gy)
+        ops, k = _lib.ops(), w.shape[2]
         if ctx.needs_input_grad[0]:
-            dx = _new_act(*x.shape, x.device)
-            if x.stride(1) == 1 and dx.stride(1) != 1:
-                dx = dx.contiguous(memory_format=CL)
-            ag, adx = _lib.act(gy), _lib.act(dx)
-            nb = L.ic_conv2d_dgrad_ws_ex(ag, k, stride, padding, adx, math)
-            buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv2d_dgrad_ex(ag, _lib.ptr(w), k, stride, padding, adx, math, _lib.ptr(buf), nb, st),
-                       "conv2d_dgrad")
+            dx = ops.conv2d_dgrad(gy, w, x, stride, padding, math)
+            _log_plan("conv2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw = torch.empty_like(w)
-            db = torch.empty(w.shape[0], device=w.device, dtype=w.dtype) if has_b else None
-            ax, ag = _lib.act(x), _lib.act(gy)
-            nb = L.ic_conv2d_wgrad_ws_ex(ax, ag, k, stride, padding, math)
-            buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv2d_wgrad_ex(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db), math,
-                                            _lib.ptr(buf), nb, st), "conv2d_wgrad")
+            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b, math)
+            _log_plan("conv2d_wgrad", x, gy, k, stride, padding, math)
+            db = db if has_b else None
         return dx, dw, db, None, None, None, None
 
 
 class ConvTranspose2dFn(Function):
-    """torch.nn.ConvTranspose2d forward/backward (synthesis.py:55-57, prior_synthesis.py:54-56).
-    output_padding is implied by `out_hw`."""
+    """torch.nn.ConvTranspose2d forward/backward (synthesis.py:55-57, prior_synthesis.py:54-56)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, output_padding, act, math=0):
         _lib.require_device(x, weight, bias)
-        L = _L()
         x = _cl(x)
         w = weight.contiguous()
         b = None if bias is None else bias.contiguous()
-        N, Cin, H, W = x.shape
-        Cin_w, Cout, k, k2 = w.shape
-        if Cin_w != Cin or k != k2:
+        if w.shape[0] != x.shape[1] or w.shape[2] != w.shape[3]:
             raise RuntimeError(f"conv_transpose2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
-        Ho = (H - 1) * stride - 2 * padding + k + output_padding
-        Wo = (W - 1) * stride - 2 * padding + k + output_padding
-        y = _new_act(N, Cout, Ho, Wo, x.device)
-        ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_conv_transpose2d_fwd_ws_ex(ax, k, stride, padding, ay, int(math))
-        buf = _ws(nb, x.device)
-        _lib.check(L.ic_conv_transpose2d_fwd_ex(ax, _lib.ptr(w), _lib.ptr(b), k, stride, padding, ay, int(act),
-                                                int(math), _lib.ptr(buf), nb, _lib.stream_of(x)),
-                   "conv_transpose2d_fwd")
-        ctx.conf = (stride, padding, k, act, b is not None, int(math))
+        y = _lib.ops().conv_transpose2d_fwd(x, w, b, stride, padding, output_padding, int(act), int(math))
+        _log_plan("conv_transpose2d_fwd", x, y, w.shape[2], stride, padding, math)
+        ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, padding, k, act, has_b, math = ctx.conf
-        L = _L()
+        stride, padding, act, has_b, math = ctx.conf
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
         dx = dw = db = None
-        st = _lib.stream_of(gy)
+        ops, k = _lib.ops(), w.shape[2]
         if ctx.needs_input_grad[0]:
-            dx = _new_act(*x.shape, x.device)
-            ag, adx = _lib.act(gy), _lib.act(dx)
-            nb = L.ic_conv_transpose2d_dgrad_ws_ex(ag, k, stride, padding, adx, math)
-            buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv_transpose2d_dgrad_ex(ag, _lib.ptr(w), k, stride, padding, adx, math,
-                                                      _lib.ptr(buf), nb, st), "conv_transpose2d_dgrad")
+            dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
+            _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw = torch.empty_like(w)
-            db = torch.empty(w.shape[1], device=w.device, dtype=w.dtype) if has_b else None
-            ax, ag = _lib.act(x), _lib.act(gy)
-            nb = L.ic_conv_transpose2d_wgrad_ws_ex(ax, ag, k, stride, padding, math)
-            buf = _ws(nb, gy.device)
-            _lib.check(L.ic_conv_transpose2d_wgrad_ex(ax, ag, k, stride, padding, _lib.ptr(dw), _lib.ptr(db), math,
-                                                   _lib.ptr(buf), nb, st), "conv_transpose2d_wgrad")
+            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b, math)
+            _log_plan("conv_transpose2d_wgrad", x, gy, k, stride, padding, math)
+            db = db if has_b else None
         return dx, dw, db, None, None, None, None, None
 
 
@@ -211,18 +195,12 @@ class GDNFn(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, inverse, math=0, math_fwd=0):
         _lib.require_device(x, gamma, beta)
-        L = _L()
         x = _cl(x)
         g = gamma.contiguous()
         b = beta.contiguous()
-        y = torch.empty_like(x)
-        norm = torch.empty_like(x)
-        ax, ay = _lib.act(x), _lib.act(y)
-        nb = L.ic_gdn_fwd_ws_ex(ax, int(math_fwd))
-        buf = _ws(nb, x.device)
-        _lib.check(L.ic_gdn_fwd_ex(ax, _lib.ptr(g), _lib.ptr(b), int(inverse), ay, _lib.ptr(norm), int(math_fwd),
-                                   _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_fwd")
-        ctx.inverse = int(inverse)
+        y, norm = _lib.ops().gdn_fwd(x, g, b, bool(inverse), int(math_fwd))
+        _log_plan("gdn_fwd", x, None, math=math_fwd)
+        ctx.inverse = bool(inverse)
         ctx.math = int(math)
         ctx.save_for_backward(x, norm, g)
         return y
@@ -230,16 +208,9 @@ class GDNFn(Function):
     @staticmethod
     def backward(ctx, gy):
         x, norm, g = ctx.saved_tensors
-        L = _L()
         gy = _match(gy, x)
-        dx = torch.empty_like(x)
-        dg = torch.empty_like(g)
-        dbeta = torch.empty(g.shape[0], device=g.device, dtype=g.dtype)
-        ax, adx = _lib.act(x), _lib.act(dx)
-        nb = L.ic_gdn_bwd_ws(ax)
-        buf = _ws(nb, x.device)
-        _lib.check(L.ic_gdn_bwd_ex(ax, _lib.ptr(norm), _lib.ptr(gy), _lib.ptr(g), ctx.inverse, adx, _lib.ptr(dg),
-                                   _lib.ptr(dbeta), ctx.math, _lib.ptr(buf), nb, _lib.stream_of(x)), "gdn_bwd")
+        dx, dg, dbeta = _lib.ops().gdn_bwd(x, norm, gy, g, ctx.inverse, ctx.math)
+        _log_plan("gdn_bwd", x, None, math=ctx.math)
         return dx, dg, dbeta, None, None, None
 
 

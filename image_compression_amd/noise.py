@@ -61,12 +61,14 @@ def device_state(device):
 
 
 def philox_stream(n, device):
-    """Reserve n counters of this step; returns (state tensor, offset)."""
+    """Reserve n elements of this step's stream; returns (state tensor, offset).
+    Reservations are whole Philox blocks (4 elements), so every draw starts at a
+    4-aligned offset and the z and y draws of a step never share a block."""
     s = _st()
     st = device_state(device)
     k = _key(device)
     off = s.offset[k]
-    s.offset[k] = off + int(n)
+    s.offset[k] = off + (int(n) + 3) // 4 * 4
     return st, off
 
 

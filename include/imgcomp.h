@@ -142,6 +142,54 @@ int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int in
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- launch-plan query: which kernel instance, tile and K / pixel split a conv or GDN op would launch
+ *      for these shapes (no launch, no device access; the same decision code as the launching entry
+ *      points).  op selects the entry point and the meaning of (a, b):
+ *        IC_OP_CONV2D_FWD   a = x,  b = y     IC_OP_TCONV_FWD    a = x,  b = y
+ *        IC_OP_CONV2D_DGRAD a = dy, b = dx    IC_OP_TCONV_DGRAD  a = dy, b = dx
+ *        IC_OP_CONV2D_WGRAD a = x,  b = dy    IC_OP_TCONV_WGRAD  a = x,  b = dy
+ *        IC_OP_GDN_FWD      a = x (b unused; k, stride, pad ignored)    IC_OP_GDN_BWD  likewise
+ *      Returns 0 and fills *out, or IC_ERR_ARG for shapes the launch would reject (including tensors
+ *      whose element offsets exceed the kernels' 32-bit indexing).  Used by the parity tests to prove
+ *      they reach the kernel instances the benchmark runs. */
+#define IC_OP_CONV2D_FWD 0
+#define IC_OP_CONV2D_DGRAD 1
+#define IC_OP_CONV2D_WGRAD 2
+#define IC_OP_TCONV_FWD 3
+#define IC_OP_TCONV_DGRAD 4
+#define IC_OP_TCONV_WGRAD 5
+#define IC_OP_GDN_FWD 6
+#define IC_OP_GDN_BWD 7
+/* kernel ids */
+#define IC_KERNEL_IG_FP32 1         /* ig_kernel: implicit GEMM on the fp32 MFMA */
+#define IC_KERNEL_IG_FP32_GATHER 2  /* ig_kernel, flattened (tap, channel) gather */
+#define IC_KERNEL_IG_BF16 3         /* ig_kernel_bf16: bf16 operands, 64-channel chunks */
+#define IC_KERNEL_IG_SPLIT 4        /* ig_kernel_x3s: fp32 by the exact three-term bf16 split */
+#define IC_KERNEL_IG_SPLIT_BF16 5   /* ig_kernel_x3s with one bf16 product (bf16 operands) */
+#define IC_KERNEL_EDGE_CONV 6       /* edge_conv_kernel: few-channel image -> wide map */
+#define IC_KERNEL_IM2COL_GEMM 7     /* im2col columns + ig_kernel */
+#define IC_KERNEL_TCONV_FEW 8       /* tconv_few_kernel: wide map -> few-channel image, output-row stationary */
+#define IC_KERNEL_TCONV_FEW_ROWS 9  /* tconv_few2_kernel: the same, input-row stationary */
+#define IC_KERNEL_GEMM_COL2IM 10    /* ig_kernel + col2im gather */
+#define IC_KERNEL_WG_FP32 11        /* wg_kernel: weight gradient on the fp32 MFMA */
+#define IC_KERNEL_WG_FP32_GATHER 12 /* wg_kernel, flattened (tap, channel) columns */
+#define IC_KERNEL_WG_LDSDMA 13      /* wg_glds_kernel: fp32 MFMA, LDS-DMA staged */
+#define IC_KERNEL_WG_SPLIT 14       /* wg_x3_kernel: weight gradient in split arithmetic */
+#define IC_KERNEL_EDGE_WGRAD 15     /* edge_wgrad_kernel */
+#define IC_KERNEL_GDN_FUSED 16      /* gdn_fwd_fused_kernel / gdn_bwd_fused_kernel (fp32 dx) */
+#define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3_kernel / gdn_bwd_fused_kernel with split dgamma */
+#define IC_KERNEL_GDN_GEMM 18       /* GDN on the implicit GEMM (+ wgrad kernel for dgamma) */
+typedef struct ic_plan {
+  int kernel;        /* IC_KERNEL_* of the main launch */
+  int bm, bn;        /* block tile: output rows (pixels; weight-gradient: G channels) x columns */
+  int ksplit;        /* implicit GEMM K splits (1 = none; > 1 adds a deterministic partial-sum pass) */
+  int nsplit;        /* weight gradient pixel splits (0 for other ops) */
+  int im2col;        /* 1 when a column buffer is materialised in HBM */
+  int variant;       /* kernel-specific template variant (weight gradient: 1 = row-fast addressing) */
+  long long blocks;  /* workgroups of the main launch (-1 when not reported) */
+} ic_plan;
+int ic_conv_plan(int op, const ic_act* a, const ic_act* b, int k, int stride, int pad, int math, ic_plan* out);
+
 /* ---- elementwise on dense storage of n elements ---- */
 /* NonNegativeParam: v = max(p, bound); out = v*v - ped */
 int ic_nonneg_fwd(const float* p, long long n, float bound, float ped, float* out, void* stream);
@@ -174,13 +222,19 @@ int ic_mse_fwd(const float* a, const float* b, long long n, float* out, void* ws
 int ic_mse_bwd(const float* a, const float* b, const float* gout, long long n, float* ga, float* gb,
                void* stream);
 
-/* ---- noise: u[i] = Philox4x32-10(seed, offset + i) -> U[0,1) ---- */
+/* ---- noise: the training-noise stream (replaces torch.rand_like of entropy_model.py:230,333).
+ *      Element i of stream `seed` is word (i & 3) of Philox4x32-10(counter {i >> 2 as 64 bits, 0, 0},
+ *      key {seed lo, seed hi}), mapped to U[0,1) by its top 24 bits: u[i] = element offset + i.
+ *      offset must be a multiple of 4 (whole Philox blocks; IC_ERR_ARG otherwise). */
 int ic_uniform(float* u, long long n, unsigned long long seed, unsigned long long offset,
                void* stream);
+/* raw Philox4x32-10 for known-answer tests: in (device) holds n items {c0, c1, c2, c3, k0, k1},
+ * out (device) receives n items {r0, r1, r2, r3} */
+int ic_philox_kat(const unsigned* in, unsigned* out, int n, void* stream);
 /* graph-safe noise stream: a device-resident state {seed, base}; quantizers in
- * mode 3 draw Philox(seed, base + offset + i).  Advancing the base by the
- * counters one training step consumed is itself a kernel, so a captured
- * hipGraph replays with fresh noise every time.  state[1] += n */
+ * mode 3 draw elements base + offset + i of stream seed.  Advancing the base by the
+ * elements one training step consumed is itself a kernel, so a captured
+ * hipGraph replays with fresh noise every time.  state[1] += n rounded up to a multiple of 4 */
 int ic_philox_advance(unsigned long long* state, unsigned long long n, void* stream);
 
 /* ---- factorized entropy model (z): C channels, elements e with channel c = idx % C

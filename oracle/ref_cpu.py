@@ -99,6 +99,26 @@ def gdn_init(C, gamma_init=0.1, offset=2.0 ** -18):
     return gp, bp
 
 
+# ---------------------------------------------------------------- ReLU ties
+def _relu(x, ctl):
+    """F.relu, or (with a control dict) a ReLU whose gradient mask is given.
+
+    ReLU's derivative jumps at 0, so a pre-activation that lies within
+    rounding error of 0 can take either side in two correct fp32
+    implementations, and the two gradients then differ by that element's
+    whole contribution.  Tests compare the HIP path with this oracle under
+    the HIP path's masks (ctl["masks"], consumed in call order) and check
+    separately that every mask the two disagree on sits on such a tie
+    (ctl["pre"] receives this oracle's pre-activations in call order)."""
+    if ctl is None:
+        return F.relu(x)
+    ctl.setdefault("pre", []).append(x.detach())
+    masks = ctl.get("masks")
+    if masks:
+        return x * masks[len(ctl["pre"]) - 1].to(x.dtype)
+    return F.relu(x)
+
+
 # ---------------------------------------------------------------- transforms
 def analysis(P, x, strides=(2, 2, 2, 2), k=5, prefix="analysis_transform.layers."):
     """modelling/blocks/analysis.py:44-71: conv(k, s, pad k//2) with GDN after
@@ -125,7 +145,7 @@ def synthesis(P, x, strides=(2, 2, 2, 2), k=5, prefix="synthesis_transform.layer
     return x
 
 
-def hyper_analysis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_analysis._layers."):
+def hyper_analysis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_analysis._layers.", relu_ctl=None):
     """modelling/blocks/prior_analysis.py:43-71: conv, ReLU, conv, ReLU, conv
     (no bias on the last conv)."""
     n = len(strides)
@@ -133,11 +153,11 @@ def hyper_analysis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_ana
         b = P.get(f"{prefix}{2*i}.bias") if i < n - 1 else None
         x = F.conv2d(x, P[f"{prefix}{2*i}.weight"], b, stride=s, padding=k // 2)
         if i < n - 1:
-            x = F.relu(x)
+            x = _relu(x, relu_ctl)
     return x
 
 
-def hyper_synthesis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_synthesis._layers."):
+def hyper_synthesis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_synthesis._layers.", relu_ctl=None):
     """modelling/blocks/prior_synthesis.py:44-72: reversed kernels/strides,
     conv_transpose + ReLU, last layer then clamp(exp(.), 1e-10, 1e10)."""
     n = len(strides)
@@ -145,7 +165,7 @@ def hyper_synthesis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_sy
         x = F.conv_transpose2d(x, P[f"{prefix}{2*i}.weight"], P[f"{prefix}{2*i}.bias"],
                                stride=s, padding=k // 2, output_padding=s - 1)
         if i < n - 1:
-            x = F.relu(x)
+            x = _relu(x, relu_ctl)
     return torch.clamp(x.exp(), 1e-10, 1e10)
 
 
@@ -337,15 +357,15 @@ def ms_ssim_metric_db(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
 # ---------------------------------------------------------------- full model
 def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             loss_names=("MSE",), lam=256.0, ssim_log=True,
-            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5)):
+            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None):
     """modelling/meta_arch/bmshl2018.py:68-98 Compressor2018.forward.
     Returns dict of intermediates and the loss dict."""
     N, C, H, W = x.shape
     num_pixels = N * H * W
     y = analysis(P, x, strides)
-    z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels)
+    z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl)
     z_tilde, p_z, ce_z = factorized(P, z, u_z, train)
-    sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels)
+    sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl)
     y_tilde, p_y = conditional(y, sigma, u_y, train, cond)
     ce_y = ce_loss(p_y)
     x_raw = synthesis(P, y_tilde, strides)

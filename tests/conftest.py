@@ -63,3 +63,39 @@ def assert_close(a, b, rtol=1e-4, name=""):
         raise AssertionError(
             f"{name}: {int(bad.sum())}/{a.size} elements off; max|d|={np.abs(a-b).max():.3e} "
             f"at {np.unravel_index(i, a.shape)} a={a.flat[i]:.6g} b={b.flat[i]:.6g} atol={atol:.3e}")
+
+
+class HipReluMasks:
+    """Records, in call order, the gradient masks (input > 0) of the HIP model's
+    hyperprior ReLUs (the only ReLUs of Compressor2018), for the oracle's
+    relu_ctl (oracle/ref_cpu.py _relu)."""
+
+    def __init__(self, model):
+        self.masks = []
+        self.handles = []
+        for blk in (model.prior_analysis, model.prior_synthesis):
+            for m in blk.modules():
+                if type(m).__name__ == "ReLU":
+                    self.handles.append(m.register_forward_hook(
+                        lambda mod, inp, out: self.masks.append((inp[0] > 0).detach().cpu())))
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+
+
+def check_relu_ties(masks, ctl, tau=1e-4):
+    """Every ReLU mask the HIP path and the oracle disagree on must sit on a tie:
+    |oracle pre-activation| <= tau * max |pre-activation| of that layer.
+    Returns the number of disagreements."""
+    assert len(masks) == len(ctl["pre"]), (len(masks), len(ctl["pre"]))
+    flips = 0
+    for i, (m, pre) in enumerate(zip(masks, ctl["pre"])):
+        pre = pre.double()
+        diff = m != (pre > 0)
+        if diff.any():
+            lim = tau * float(pre.abs().max())
+            worst = float(pre[diff].abs().max())
+            assert worst <= lim, f"ReLU {i}: mask differs at |pre| = {worst:.3e} > {lim:.3e}"
+            flips += int(diff.sum())
+    return flips

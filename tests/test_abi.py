@@ -91,3 +91,91 @@ def test_yaml_configs_merge(tmp_path):
     assert cfg.MODEL.LOSS.DISTORTION_LOSS_NAMES == ["MS_SSIMLoss"]
     assert cfg.MODEL.LOSS.SSIM.LOG_SCALE is True
     assert cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT == 64.0
+
+
+def test_modelling_alias_imports_reference_style():
+    """`import modelling` (the reference's package name, engine/trainer.py:248-261) yields
+    the same module objects as image_compression_amd.modelling."""
+    import modelling
+    from modelling import build_model
+    from modelling.layers import GDN
+    from modelling.meta_arch import META_ARCH_REGISTRY
+    import image_compression_amd.modelling as real
+    assert modelling is real
+    assert build_model is real.build_model and GDN is real.layers.GDN
+    assert META_ARCH_REGISTRY is real.meta_arch.META_ARCH_REGISTRY
+
+
+def _act(n, c, h, w, cl=True, data=256):
+    from image_compression_amd import _lib
+    if cl:
+        return _lib.ICAct(data, n, c, h, w, c * h * w, 1, w * c, c)
+    return _lib.ICAct(data, n, c, h, w, c * h * w, h * w, w, 1)
+
+
+def test_plan_query_c2_instances():
+    """ic_conv_plan (no launch): the kernel instances the C2 benchmark batch takes."""
+    from image_compression_amd import _lib
+    x, y = _act(32, 192, 128, 128), _act(32, 192, 64, 64)
+    p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 2)
+    assert (p["kernel"], p["bm"], p["bn"], p["ksplit"]) == ("ig_split", 128, 192, 1)
+    assert p["blocks"] == 32 * 64 * 64 // 128
+    p = _lib.plan("conv2d_dgrad", y, x, 5, 2, 2, 2)
+    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split", 128, 1)
+    p = _lib.plan("conv2d_wgrad", x, y, 5, 2, 2, 2)
+    assert (p["kernel"], p["variant"]) == ("wg_split", 1) and p["nsplit"] >= 1
+    p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 0)
+    assert p["kernel"] == "ig_fp32"
+    p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 1)
+    assert p["kernel"] == "ig_bf16"
+    # small maps: 64-row tiles with split-K
+    p = _lib.plan("conv2d_fwd", _act(32, 192, 16, 16), _act(32, 192, 8, 8), 5, 2, 2, 2)
+    assert (p["kernel"], p["bm"]) == ("ig_split", 64) and p["ksplit"] > 1
+    # image edges and GDN
+    img = _act(32, 3, 256, 256, cl=False)
+    assert _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 2)["kernel"] == "edge_conv"
+    assert _lib.plan("conv_transpose2d_fwd", x, img, 5, 2, 2, 2)["kernel"] == "tconv_few_rows"
+    assert _lib.plan("gdn_fwd", x, math=2)["kernel"] == "gdn_fused_split"
+    assert _lib.plan("gdn_bwd", x, math=0)["kernel"] == "gdn_fused"
+
+
+def test_extent_guard_rejects_32bit_overflow():
+    """Tensors whose element offsets reach 2^31 are rejected (IC_ERR_ARG), not wrapped."""
+    from image_compression_amd import _lib
+    L = _lib.load()
+    big = _act(1024, 192, 512, 512)       # 5.2e10 elements
+    out = _act(1024, 192, 256, 256)
+    with pytest.raises(RuntimeError, match="1001"):
+        _lib.plan("conv2d_fwd", big, out, 5, 2, 2, 2)
+    with pytest.raises(RuntimeError, match="1001"):
+        _lib.plan("conv2d_wgrad", big, out, 5, 2, 2, 2)
+    with pytest.raises(RuntimeError, match="1001"):
+        _lib.plan("conv_transpose2d_fwd", out, big, 5, 2, 2, 2)
+    with pytest.raises(RuntimeError, match="1001"):
+        _lib.plan("gdn_fwd", big, math=2)
+    assert L.ic_conv2d_fwd_ws_ex(big, 5, 2, 2, out, 2) == 0   # the workspace query reports failure as 0
+    # just below the limit is accepted: 2^31 - 1 addressable elements
+    ok = _act(43, 192, 512, 512)          # 2.16e9 > 2^31 -> rejected
+    ok2 = _act(42, 192, 512, 512)         # 2.11e9 < 2^31
+    with pytest.raises(RuntimeError):
+        _lib.plan("gdn_fwd", ok, math=2)
+    assert _lib.plan("gdn_fwd", ok2, math=2)["kernel"] == "gdn_fused_split"
+
+
+def test_torch_ops_registered_with_shape_kernels():
+    """torch.ops.imgcomp.* (TORCH_LIBRARY, csrc/torch_ops.cpp) load and infer shapes on the meta device."""
+    from image_compression_amd import _lib
+    ops = _lib.ops()
+    x = torch.empty(2, 192, 32, 32, device="meta").contiguous(memory_format=torch.channels_last)
+    w = torch.empty(192, 192, 5, 5, device="meta")
+    y = ops.conv2d_fwd(x, w, None, 2, 2, 0, 2)
+    assert y.shape == (2, 192, 16, 16) and y.is_contiguous(memory_format=torch.channels_last)
+    assert ops.conv2d_dgrad(y, w, x, 2, 2, 2).shape == x.shape
+    dw, db = ops.conv2d_wgrad(x, y, w, 2, 2, True, 2)
+    assert dw.shape == w.shape and db.shape == (192,)
+    assert ops.conv_transpose2d_fwd(y, w, None, 2, 2, 1, 0, 2).shape == x.shape
+    yy, nn = ops.gdn_fwd(x, torch.empty(192, 192, device="meta"), torch.empty(192, device="meta"), False, 2)
+    assert yy.shape == nn.shape == x.shape
+    for name in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "conv_transpose2d_fwd", "conv_transpose2d_dgrad",
+                 "conv_transpose2d_wgrad", "gdn_fwd", "gdn_bwd"):
+        assert hasattr(ops, name), name
