@@ -12,7 +12,7 @@ output pixels, i.e. at the BASELINE configurations' batch sizes.  These tests
     launches (recorded through functional.record_plans on a bench-size step)
     was launched by the test step.  The oracle takes the HIP path's
     hyperprior ReLU masks; a mask may differ only where the pre-activation is
-    a tie (|pre| <= 1e-4 max|pre|; conftest.check_relu_ties).
+    a tie (|pre| <= 1e-4 max|pre|, 2e-2 with bf16 operands; conftest.check_relu_ties).
 Reference: modelling/meta_arch/bmshl2018.py:68-98 (the step), analysis.py:55 /
 synthesis.py:55 (the layers)."""
 import numpy as np
@@ -171,7 +171,9 @@ def test_config_step_vs_oracle_and_bench_plans(name):
     if loss == "msssim":
         kw.update(loss_names=("MS_SSIMLoss",), ssim_log=True)
     out, ref_losses, ref_grads = ref_cpu.run(params, x, uz, uy, train=True, dtype=torch.float64, **kw)
-    flips = check_relu_ties(hm.masks, ctl)
+    # bf16 operands (C3) move y by ~1e-2 normwise, so h_a's pre-activations differ from the fp64
+    # oracle's by up to ~1e-2 of their range: a mask flip there is a tie at that scale
+    flips = check_relu_ties(hm.masks, ctl, tau=2e-2 if dtype == "bf16" else 1e-4)
     errs = {k: rel_err(p.grad.cpu(), ref_grads[k]) for k, p in model.named_parameters()}
     worst = sorted(((e, k) for k, e in errs.items()), reverse=True)[:5]
     print(f"{name}: x_tilde {rel_err(xt.cpu(), out['x_tilde'].detach()):.2e}; ReLU ties {flips}; worst grads {worst}")
