@@ -66,6 +66,18 @@ MATH_NOTE = {
 BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
 
 
+def _bound_spec(math):
+    """Spec bound (TFLOP/s of the config's algorithmic work) of the arithmetic `math` runs on."""
+    return {"fp32": FP32_PEAK_TFLOPS, "fp32_split": BF16_PEAK_TFLOPS / 6, "bf16": BF16_PEAK_TFLOPS}[math]
+
+
+def _frac_measured(tflops, math):
+    pm = _mfma_peak_measured()
+    if not pm or math not in pm["bound_tflops"]:
+        return None
+    return round(tflops / pm["bound_tflops"][math], 4)
+
+
 def _cfg(lam=256.0, conf=None):
     from image_compression_amd import get_cfg_defaults
     cfg = get_cfg_defaults()
@@ -106,6 +118,7 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     iso_ms = e0.elapsed_time(e1) / reps
     ms = live_ms if live_ms else iso_ms
     achieved = flop / (ms * 1e-3) / 1e12
+    pm = _mfma_peak_measured()
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
         peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,true,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
@@ -121,7 +134,9 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
             "timing": (f"live: HIP events on the launch stream around the layer's {live_launches} launches "
                        "inside the timed steps" if live_ms else "isolated loop of the same launch"),
             "isolated_ms_per_launch": round(iso_ms, 4),
-            "peak_measured": _mfma_peak_measured()}
+            "peak_measured": pm,
+            "frac_of_measured_peak": (round(achieved / pm["bound_tflops"][math], 4)
+                                      if pm and math in pm["bound_tflops"] else None)}
 
 
 class LiveLaunchTimer:
@@ -199,16 +214,26 @@ def _pmc_traffic(kernel):
 
 
 def _mfma_peak_measured():
-    """Sustained fp32 MFMA rate measured on the box by tools/mfma_peak.hip
-    (committed as profiles/*_mfma_peak.json; SURVEY.md 8d: report the spec
-    peak and the measured one)."""
+    """Sustained MFMA rates measured on an MI355X by tools/mfma_peak.hip (committed as
+    profiles/*_mfma_peak.json; SURVEY.md 8d: report the spec peak and the measured one):
+    v_mfma_f32_32x32x2_f32 and, on RANDOM operands (the chip holds a lower clock on random
+    bf16 data than the spec assumes), v_mfma_f32_16x16x32_bf16 -- the instruction the
+    fp32_split kernels run six of per fp32 MAC, so the measured split bound is its rate / 6."""
     import glob
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_mfma_peak.json")))
     if not files:
         return None
     with open(files[-1]) as fh:
         rows = [json.loads(line) for line in fh if line.strip()]
-    return max(r["tflops"] for r in rows) if rows else None
+    fp32 = max((r["tflops"] for r in rows if "f32_32x32x2" in r.get("instr", "v_mfma_f32_32x32x2_f32")), default=None)
+    bf16 = max((r["tflops"] for r in rows if "16x16x32_bf16" in r.get("instr", "")), default=None)
+    out = {"file": os.path.relpath(files[-1], HERE), "fp32_mfma_tflops": fp32,
+           "bf16_16x16x32_random_tflops": bf16, "bound_tflops": {}}
+    if fp32:
+        out["bound_tflops"]["fp32"] = fp32
+    if bf16:
+        out["bound_tflops"]["fp32_split"] = round(bf16 / 6, 2)
+    return out
 
 
 def cpu_baseline(seconds_target=12.0):
@@ -345,7 +370,10 @@ def main():
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(step_tflops, 2),
-            "model_mfma_frac": round(step_tflops / FP32_PEAK_TFLOPS, 4),
+            # the whole step's algorithmic fp32 FLOP/s over the bound of the arithmetic it runs on:
+            # fp32_split -> bf16 MFMA spec / 6 (and the measured random-operand rate / 6); fp32 -> fp32 MFMA
+            "model_frac_of_bound": round(step_tflops / _bound_spec(conf["math"]), 4),
+            "model_frac_of_measured_bound": _frac_measured(step_tflops, conf["math"]),
             "bpp": round(bpp, 4), dname.lower(): dist_val,
             "optimizer_step_ms": opt_ms,
             "images_256_equiv_per_s": round(value * (args.size / 256) ** 2, 2),
