@@ -34,6 +34,18 @@ class ICFactGrads(ctypes.Structure):
     _fields_ = [(f, c_void) for f in _FACT_FIELDS]
 
 
+FACT_MAXL, FACT_MAXW = 6, 8  # IC_FACT_MAXL / IC_FACT_MAXW
+
+
+class ICFactNet(ctypes.Structure):
+    _fields_ = [("nlayers", c_int), ("dims", c_int * (FACT_MAXL + 1)), ("w", c_void * FACT_MAXL),
+                ("b", c_void * FACT_MAXL), ("f", c_void * FACT_MAXL)]
+
+
+class ICFactNetGrads(ctypes.Structure):
+    _fields_ = [("w", c_void * FACT_MAXL), ("b", c_void * FACT_MAXL), ("f", c_void * FACT_MAXL)]
+
+
 class ICAdamWTensor(ctypes.Structure):
     _fields_ = [("param", c_void), ("grad", c_void), ("exp_avg", c_void), ("exp_avg_sq", c_void),
                 ("n", c_ll), ("lr", c_float), ("weight_decay", c_float)]
@@ -115,6 +127,14 @@ SIGNATURES = {
     "ic_factorized_bwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_void, c_void, c_void, P(ICFactGrads), c_void]),
     "ic_conditional_fwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),
     "ic_conditional_bwd": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_void, c_void, c_void, c_void, c_void, c_void]),
+    "ic_conditional_fwd_bin": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_int, c_void, c_ull, c_ull, c_float,
+                                       c_void, c_void, c_void]),
+    "ic_conditional_bwd_bin": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_float, c_void, c_void, c_void, c_void,
+                                       c_void, c_void]),
+    "ic_factorized_fwd_net": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_int, c_void, c_ull, c_ull, c_void,
+                                      c_void, c_void]),
+    "ic_factorized_bwd_net": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_void, c_void, c_void,
+                                      P(ICFactNetGrads), c_void]),
     "ic_msssim_state_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "ic_msssim_ws": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "ic_msssim_fwd": (c_int, [c_void, c_void, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int,

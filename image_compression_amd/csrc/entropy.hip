@@ -235,19 +235,21 @@ __device__ __forceinline__ float dcdf_gauss(float v) {
 }
 
 __device__ __forceinline__ void cond_elem(const float* y, const float* sc, const float* mean, long long i, int kind,
-                                          float uu, int mode, float* qo, float* po) {
-  const float qv = mode == 1 ? rintf(y[i]) : y[i] + (uu - 0.5f);
+                                          float uu, int mode, float half, float* qo, float* po) {
+  // noise u - bin/2 (entropy_model.py:331-334), round (:336), mass over +-bin/2 (:347-350)
+  const float qv = mode == 1 ? rintf(y[i]) : y[i] + (uu - half);
   qo[i] = qv;
   const float a = fabsf(qv - (mean ? mean[i] : 0.f));
   const float s = sc[i];
-  const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
+  const float vu = (half - a) / s, vl = (-half - a) / s;
   po[i] = kind == 0 ? cdf_lap(vu) - cdf_lap(vl) : cdf_gauss(vu) - cdf_gauss(vl);
 }
 
 // one quad of elements per thread and iteration: in the Philox modes one Philox block
 // (four uniforms) serves the quad (stream offsets are 4-aligned)
 __global__ void cond_fwd_k(const float* y, const float* sc, const float* mean, long long n, int kind, int mode,
-                           const float* u, unsigned long long seed, unsigned long long off, float* qo, float* po) {
+                           const float* u, unsigned long long seed, unsigned long long off, float half, float* qo,
+                           float* po) {
   const long long nq = (n + 3) >> 2;
   for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq; j += (long long)gridDim.x * blockDim.x) {
     floatx4v r = {0.f, 0.f, 0.f, 0.f};
@@ -260,18 +262,18 @@ __global__ void cond_fwd_k(const float* y, const float* sc, const float* mean, l
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const long long i = 4 * j + e;
-      if (i < n) cond_elem(y, sc, mean, i, kind, mode == 0 ? u[i] : r[e], mode, qo, po);
+      if (i < n) cond_elem(y, sc, mean, i, kind, mode == 0 ? u[i] : r[e], mode, half, qo, po);
     }
   }
 }
 
-__global__ void cond_bwd_k(const float* q, const float* sc, const float* mean, long long n, int kind,
+__global__ void cond_bwd_k(const float* q, const float* sc, const float* mean, long long n, int kind, float half,
                            const float* dq, const float* dp, float* dy, float* ds, float* dm) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float d = q[i] - (mean ? mean[i] : 0.f);
     const float a = fabsf(d);
     const float s = sc[i];
-    const float vu = (0.5f - a) / s, vl = (-0.5f - a) / s;
+    const float vu = (half - a) / s, vl = (-half - a) / s;
     const float g = dp ? dp[i] : 0.f;
     const float fu = kind == 0 ? dcdf_lap(vu) : dcdf_gauss(vu);
     const float fl = kind == 0 ? dcdf_lap(vl) : dcdf_gauss(vl);
@@ -283,6 +285,268 @@ __global__ void cond_bwd_k(const float* q, const float* sc, const float* mean, l
     if (ds) ds[i] = gs;
     if (dm) dm[i] = -gd;
   }
+}
+
+// ---------------------------------------------------------------- generic factorized model
+// Any CDF MLP widths (cfg.MODEL.ENTROPY_MODEL.DIMS: hidden widths <= IC_FACT_MAXW,
+// len(DIMS) + 1 <= IC_FACT_MAXL layers; entropy_model.py:88-99) and any BIN
+// (noise u - bin/2, mass over +-bin/2: :229-232, :259-269).  One block per
+// channel; the channel's transformed parameters (softplus W, b, tanh f) sit in
+// LDS.  Every loop runs to the compile-time maxima under a width predicate, so
+// activations stay in registers.  Backward: per round of FE elements, thread t
+// backpropagates evaluation t & 1 (lower / upper) of element t >> 1 and writes
+// its per-layer terms -- delta = dL/da, the gate term dL/dh * tanh(a), the
+// layer input h -- to LDS row t; then each thread sums its own parameters' terms
+// over the round's rows in row order (deterministic, no atomics).
+constexpr int FMW = IC_FACT_MAXW, FML = IC_FACT_MAXL;
+constexpr int FNT = 128;             // threads per block (FNT / 2 elements per round)
+constexpr int FPJ = (FML * (FMW * FMW + 2 * FMW) + FNT - 1) / FNT;  // parameters per thread
+
+struct FactLayout {  // offsets of layer l's softplus(W) [dout][din], b [dout], tanh(f) [dout] in LDS
+  int ow[FML], ob[FML], of[FML], nprm;
+  int rd[FML], rg[FML], rh[FML], nrow;  // row offsets of delta, gate term, layer input
+};
+
+__device__ __forceinline__ void fact_layout(const ic_fact_net& N, FactLayout& F) {
+  int o = 0, r = 0;
+#pragma unroll
+  for (int l = 0; l < FML; ++l) {
+    const int din = l < N.nlayers ? N.dims[l] : 0, dout = l < N.nlayers ? N.dims[l + 1] : 0;
+    F.ow[l] = o; o += dout * din;
+    F.ob[l] = o; o += dout;
+    F.of[l] = o; o += (l < N.nlayers - 1) ? dout : 0;
+    F.rd[l] = r; r += dout;
+    F.rg[l] = r; r += dout;
+    F.rh[l] = r; r += din;
+  }
+  F.nprm = o;
+  F.nrow = r;
+}
+
+// the channel's parameters, transformed, into LDS (softplus W, b, tanh f)
+__device__ __forceinline__ void fact_load_lds(const ic_fact_net& N, const FactLayout& F, int c, float* prm) {
+  for (int l = 0; l < N.nlayers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    for (int j = threadIdx.x; j < dout * din; j += blockDim.x) prm[F.ow[l] + j] = softplusf(N.w[l][c * dout * din + j]);
+    for (int j = threadIdx.x; j < dout; j += blockDim.x) {
+      prm[F.ob[l] + j] = N.b[l][c * dout + j];
+      if (l < N.nlayers - 1) prm[F.of[l] + j] = tanhf(N.f[l][c * dout + j]);
+    }
+  }
+}
+
+// logits of one evaluation at v; REC keeps the pre-gate values A and the layer inputs H
+template <bool REC>
+__device__ __forceinline__ float fact_eval(const ic_fact_net& N, const FactLayout& F, const float* prm, float v,
+                                           float (&A)[FML][FMW], float (&H)[FML][FMW]) {
+  float h[FMW];
+#pragma unroll
+  for (int i = 0; i < FMW; ++i) h[i] = i == 0 ? v : 0.f;
+#pragma unroll
+  for (int l = 0; l < FML; ++l) {
+    if (l >= N.nlayers) break;
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    const bool gate = l < N.nlayers - 1;
+    float hn[FMW];
+#pragma unroll
+    for (int o = 0; o < FMW; ++o) {
+      hn[o] = 0.f;
+      if (o < dout) {
+        float s = prm[F.ob[l] + o];
+#pragma unroll
+        for (int i = 0; i < FMW; ++i)
+          if (i < din) s += prm[F.ow[l] + o * din + i] * h[i];
+        if (REC) A[l][o] = s;
+        hn[o] = gate ? s + tanhf(s) * prm[F.of[l] + o] : s;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FMW; ++i) {
+      if (REC) H[l][i] = h[i];
+      h[i] = hn[i];
+    }
+  }
+  return h[0];
+}
+
+__global__ void fact_fwd_net_k(const float* z, long long n, int C, const ic_fact_net N, float half, int mode,
+                               const float* u, unsigned long long seed, unsigned long long off, float* qo, float* po) {
+  extern __shared__ float flds[];
+  const int c = blockIdx.x;
+  FactLayout F;
+  fact_layout(N, F);
+  fact_load_lds(N, F, c, flds);
+  __syncthreads();
+  float A[FML][FMW], H[FML][FMW];
+  const long long ne = n / C;
+  for (long long e = threadIdx.x; e < ne; e += blockDim.x) {
+    const long long i = e * C + c;
+    float qv;
+    if (mode == 1) {
+      qv = rintf(z[i]);
+    } else {
+      float uu;
+      if (mode == 0) uu = u[i];
+      else if (mode == 3) {
+        const unsigned long long* st = (const unsigned long long*)u;
+        uu = philox_uniform(st[0], st[1] + off + (unsigned long long)i);
+      } else {
+        uu = philox_uniform(seed, off + (unsigned long long)i);
+      }
+      qv = z[i] + (uu - half);
+    }
+    qo[i] = qv;
+    const float lo = fact_eval<false>(N, F, flds, qv - half, A, H);
+    const float up = fact_eval<false>(N, F, flds, qv + half, A, H);
+    const float s = -signf_(lo + up);
+    po[i] = s * (sigmoidf_(up * s) - sigmoidf_(lo * s));
+  }
+}
+
+__global__ void __launch_bounds__(FNT) fact_bwd_net_k(const float* qin, long long n, int C, const ic_fact_net N,
+                                                      float half, const float* dq, const float* dp, float* dz,
+                                                      const ic_fact_net_grads GR) {
+  extern __shared__ float flds[];
+  const int c = blockIdx.x, t = threadIdx.x;
+  FactLayout F;
+  fact_layout(N, F);
+  float* prm = flds;
+  float* rows = flds + F.nprm;           // [FNT][nrow]
+  float* dvb = rows + FNT * F.nrow;      // [FNT] input gradients of the two evaluations
+  fact_load_lds(N, F, c, prm);
+  // the parameters this thread owns: index j = t + FNT k; term = row[oa] * (ob < 0 ? 1 : row[ob])
+  int oa[FPJ], ob[FPJ];
+  float acc[FPJ];
+#pragma unroll
+  for (int k = 0; k < FPJ; ++k) {
+    acc[k] = 0.f;
+    oa[k] = -1;
+    ob[k] = -1;
+    int j = t + FNT * k;
+    for (int l = 0; l < N.nlayers && oa[k] < 0; ++l) {
+      const int din = N.dims[l], dout = N.dims[l + 1];
+      const int nl = dout * din + dout + (l < N.nlayers - 1 ? dout : 0);
+      if (j >= nl) { j -= nl; continue; }
+      if (j < dout * din) { oa[k] = F.rd[l] + j / din; ob[k] = F.rh[l] + j % din; }
+      else if (j < dout * din + dout) { oa[k] = F.rd[l] + (j - dout * din); }
+      else { oa[k] = F.rg[l] + (j - dout * din - dout); }
+    }
+  }
+  __syncthreads();
+  float A[FML][FMW], H[FML][FMW];
+  const long long ne = n / C;
+  const int which = t & 1;  // 0: lower (q - half), 1: upper (q + half)
+  for (long long e0 = 0; e0 < ne; e0 += FNT / 2) {
+    const long long e = e0 + (t >> 1);
+    float* row = rows + t * F.nrow;
+    float dv = 0.f;
+    const bool live = e < ne;
+    const long long i = e * C + c;
+    const float gp = (live && dp) ? dp[i] : 0.f;
+    if (live && gp != 0.f) {
+      const float qv = qin[i];
+      float A2[FML][FMW], H2[FML][FMW];
+      const float lo = fact_eval<true>(N, F, prm, qv - half, which ? A2 : A, which ? H2 : H);
+      const float up = fact_eval<true>(N, F, prm, qv + half, which ? A : A2, which ? H : H2);
+      const float s = -signf_(lo + up);
+      const float su = sigmoidf_(s * up), sl = sigmoidf_(s * lo);
+      // p = s (sig(s up) - sig(s lo)), s detached
+      float g = which ? gp * s * su * (1.f - su) * s : -gp * s * sl * (1.f - sl) * s;
+      float dh[FMW];
+#pragma unroll
+      for (int o = 0; o < FMW; ++o) dh[o] = o == 0 ? g : 0.f;
+#pragma unroll
+      for (int l = FML - 1; l >= 0; --l) {
+        if (l >= N.nlayers) continue;
+        const int din = N.dims[l], dout = N.dims[l + 1];
+        const bool gate = l < N.nlayers - 1;
+        float da[FMW];
+#pragma unroll
+        for (int o = 0; o < FMW; ++o) {
+          da[o] = 0.f;
+          if (o < dout) {
+            if (gate) {
+              const float th = tanhf(A[l][o]);
+              da[o] = dh[o] * (1.f + (1.f - th * th) * prm[F.of[l] + o]);
+              row[F.rg[l] + o] = dh[o] * th;
+            } else {
+              da[o] = dh[o];
+              row[F.rg[l] + o] = 0.f;
+            }
+            row[F.rd[l] + o] = da[o];
+          }
+        }
+#pragma unroll
+        for (int i2 = 0; i2 < FMW; ++i2) {
+          float sacc = 0.f;
+          if (i2 < din) {
+            row[F.rh[l] + i2] = H[l][i2];
+#pragma unroll
+            for (int o = 0; o < FMW; ++o)
+              if (o < dout) sacc += prm[F.ow[l] + o * din + i2] * da[o];
+          }
+          dh[i2] = sacc;
+        }
+      }
+      dv = dh[0];
+    } else {
+      for (int r = 0; r < F.nrow; ++r) row[r] = 0.f;
+    }
+    dvb[t] = dv;
+    __syncthreads();
+    if (live && which == 0 && dz) dz[i] = (dq ? dq[i] : 0.f) + (dvb[t] + dvb[t + 1]);
+#pragma unroll
+    for (int k = 0; k < FPJ; ++k) {
+      if (oa[k] < 0) continue;
+      float sacc = 0.f;
+      for (int r = 0; r < FNT; ++r) {
+        const float* rr = rows + r * F.nrow;
+        sacc += ob[k] < 0 ? rr[oa[k]] : rr[oa[k]] * rr[ob[k]];
+      }
+      acc[k] += sacc;
+    }
+    __syncthreads();
+  }
+  // raw sums -> parameter gradients (softplus' for W, 1 - tanh^2 for f)
+#pragma unroll
+  for (int k = 0; k < FPJ; ++k) {
+    if (oa[k] < 0) continue;
+    int j = t + FNT * k;
+    for (int l = 0; l < N.nlayers; ++l) {
+      const int din = N.dims[l], dout = N.dims[l + 1];
+      const int nl = dout * din + dout + (l < N.nlayers - 1 ? dout : 0);
+      if (j >= nl) { j -= nl; continue; }
+      if (j < dout * din) {
+        GR.w[l][c * dout * din + j] = acc[k] * dsoftplusf(N.w[l][c * dout * din + j]);
+      } else if (j < dout * din + dout) {
+        GR.b[l][c * dout + (j - dout * din)] = acc[k];
+      } else {
+        const int o = j - dout * din - dout;
+        const float tf = tanhf(N.f[l][c * dout + o]);
+        GR.f[l][c * dout + o] = acc[k] * (1.f - tf * tf);
+      }
+      break;
+    }
+  }
+}
+
+bool fact_net_ok(const ic_fact_net* N) {
+  if (!N || N->nlayers < 1 || N->nlayers > FML || N->dims[0] != 1 || N->dims[N->nlayers] != 1) return false;
+  for (int l = 0; l < N->nlayers; ++l) {
+    if (N->dims[l + 1] < 1 || N->dims[l + 1] > FMW || !N->w[l] || !N->b[l]) return false;
+    if (l < N->nlayers - 1 && !N->f[l]) return false;
+  }
+  return true;
+}
+
+size_t fact_net_lds(const ic_fact_net* N, bool bwd) {
+  int prm = 0, row = 0;
+  for (int l = 0; l < N->nlayers; ++l) {
+    const int din = N->dims[l], dout = N->dims[l + 1];
+    prm += dout * din + dout + (l < N->nlayers - 1 ? dout : 0);
+    row += 2 * dout + din;
+  }
+  return ((size_t)prm + (bwd ? (size_t)FNT * row + FNT : 0)) * sizeof(float);
 }
 
 }  // namespace
@@ -306,27 +570,63 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
   return IC_OK;
 }
 
-int ic_conditional_fwd(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
-                       const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
-                       void* stream) {
+int ic_conditional_fwd_bin(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
+                           const float* u, unsigned long long seed, unsigned long long offset, float bin, float* q,
+                           float* p, void* stream) {
   if (mode == 0 && !u) return IC_ERR_ARG;
+  if (!(bin > 0.f)) return IC_ERR_ARG;
   if (mode == 2 && (offset & 3)) return IC_ERR_ARG;  // stream offsets are whole Philox blocks
   long long b = (n + 1023) / 1024;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
   hipLaunchKernelGGL(cond_fwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, y, scale, mean, n, kind,
-                     mode, u, seed, offset, q, p);
+                     mode, u, seed, offset, 0.5f * bin, q, p);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_conditional_fwd(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
+                       const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                       void* stream) {
+  return ic_conditional_fwd_bin(y, scale, mean, n, kind, mode, u, seed, offset, 1.f, q, p, stream);
+}
+
+int ic_conditional_bwd_bin(const float* q, const float* scale, const float* mean, long long n, int kind, float bin,
+                           const float* dq, const float* dp, float* dy, float* dscale, float* dmean, void* stream) {
+  if (!(bin > 0.f)) return IC_ERR_ARG;
+  long long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(cond_bwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, q, scale, mean, n, kind,
+                     0.5f * bin, dq, dp, dy, dscale, dmean);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
 
 int ic_conditional_bwd(const float* q, const float* scale, const float* mean, long long n, int kind,
                        const float* dq, const float* dp, float* dy, float* dscale, float* dmean, void* stream) {
-  long long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  hipLaunchKernelGGL(cond_bwd_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, q, scale, mean, n, kind,
-                     dq, dp, dy, dscale, dmean);
+  return ic_conditional_bwd_bin(q, scale, mean, n, kind, 1.f, dq, dp, dy, dscale, dmean, stream);
+}
+
+int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
+                          const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                          void* stream) {
+  if (C <= 0 || n % C != 0 || (mode == 0 && !u) || !fact_net_ok(net) || !(bin > 0.f)) return IC_ERR_ARG;
+  hipLaunchKernelGGL(fact_fwd_net_k, dim3(C), dim3(FNT), fact_net_lds(net, false), (hipStream_t)stream, z, n, C,
+                     *net, 0.5f * bin, mode, u, seed, offset, q, p);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
+int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
+                          const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream) {
+  if (C <= 0 || n % C != 0 || !fact_net_ok(net) || !grd || !(bin > 0.f)) return IC_ERR_ARG;
+  for (int l = 0; l < net->nlayers; ++l)
+    if (!grd->w[l] || !grd->b[l] || (l < net->nlayers - 1 && !grd->f[l])) return IC_ERR_ARG;
+  const size_t lds = fact_net_lds(net, true);
+  if (lds > 160 * 1024) return IC_ERR_ARG;
+  hipLaunchKernelGGL(fact_bwd_net_k, dim3(C), dim3(FNT), lds, (hipStream_t)stream, q, n, C, *net, 0.5f * bin, dq, dp,
+                     dz, *grd);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }

@@ -443,11 +443,80 @@ class FactorizedFn(Function):
         return (_from_last(dz), None, None, None, None, *grads)
 
 
+def _fact_net(dims, params):
+    """ic_fact_net for CDF layers of widths `dims` (1, DIMS..., 1) and their flat params
+    [w0, b0, f0, w1, b1, f1, ..., w_last, b_last] (CDFEstimator.flat_params order)."""
+    net = _lib.ICFactNet()
+    L = len(dims) - 1
+    net.nlayers = L
+    for i, d in enumerate(dims):
+        net.dims[i] = int(d)
+    k = 0
+    for layer in range(L):
+        net.w[layer] = params[k].data_ptr()
+        net.b[layer] = params[k + 1].data_ptr()
+        k += 2
+        if layer < L - 1:
+            net.f[layer] = params[k].data_ptr()
+            k += 1
+    return net
+
+
+class FactorizedNetFn(Function):
+    """EntropyModel with any CDF MLP widths (cfg DIMS) and any BIN (entropy_model.py:88-99,
+    :198, :229-232, :259-269) on the generic kernels (ic_factorized_*_net)."""
+
+    @staticmethod
+    def forward(ctx, z, mode, u, seed, offset, dims, bin_, *params):
+        _lib.require_device(z, None if mode == 3 else u, *params)
+        if len(dims) - 1 > _lib.FACT_MAXL or max(dims[1:-1] or [1]) > _lib.FACT_MAXW:
+            raise NotImplementedError(f"CDF MLP dims {list(dims)}: the generic kernel takes <= {_lib.FACT_MAXL} "
+                                      f"layers of width <= {_lib.FACT_MAXW}")
+        C = z.shape[1]
+        zl = _to_last(z)
+        ul = u if (u is None or mode == 3) else _to_last(u.to(z.dtype))
+        q = torch.empty_like(zl)
+        p = torch.empty_like(zl)
+        prm = [t.contiguous() for t in params]
+        net = _fact_net(dims, prm)
+        _lib.check(_L().ic_factorized_fwd_net(_lib.ptr(zl), _n(zl), C, ctypes.byref(net), float(bin_), int(mode),
+                                              _lib.ptr(ul), ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset),
+                                              _lib.ptr(q), _lib.ptr(p), _lib.stream_of(z)), "factorized_fwd_net")
+        ctx.conf = (int(mode), C, tuple(dims), float(bin_))
+        ctx.save_for_backward(q, *prm)
+        return _from_last(q), _from_last(p)
+
+    @staticmethod
+    def backward(ctx, gq, gp):
+        q, *prm = ctx.saved_tensors
+        mode, C, dims, bin_ = ctx.conf
+        gql = None if gq is None else _to_last(gq)
+        gpl = None if gp is None else _to_last(gp)
+        dz = torch.empty_like(q)
+        grads = [torch.empty_like(t) for t in prm]
+        net = _fact_net(dims, prm)
+        g = _lib.ICFactNetGrads()
+        k = 0
+        for layer in range(len(dims) - 1):
+            g.w[layer] = grads[k].data_ptr()
+            g.b[layer] = grads[k + 1].data_ptr()
+            k += 2
+            if layer < len(dims) - 2:
+                g.f[layer] = grads[k].data_ptr()
+                k += 1
+        _lib.check(_L().ic_factorized_bwd_net(_lib.ptr(q), _n(q), C, ctypes.byref(net), bin_,
+                                              None if mode == 1 else _lib.ptr(gql), _lib.ptr(gpl), _lib.ptr(dz),
+                                              ctypes.byref(g), _lib.stream_of(q)), "factorized_bwd_net")
+        if mode == 1:  # torch.round has zero gradient
+            dz.zero_()
+        return (_from_last(dz), None, None, None, None, None, None, *grads)
+
+
 class ConditionalFn(Function):
     """SymmetricConditionalModel._quantize + _prob_mass (entropy_model.py:319-352)."""
 
     @staticmethod
-    def forward(ctx, y, scale, mean, kind, mode, u, seed, offset):
+    def forward(ctx, y, scale, mean, kind, mode, u, seed, offset, bin_=1.0):
         _lib.require_device(y, scale, mean, None if mode == 3 else u)
         L = _L()
         y = _dense(y)
@@ -458,36 +527,38 @@ class ConditionalFn(Function):
             u = _match(u.to(y.dtype), y)
         q = torch.empty_like(y)
         p = torch.empty_like(y)
-        _lib.check(L.ic_conditional_fwd(_lib.ptr(y), _lib.ptr(scale), _lib.ptr(mean), _n(y), int(kind), int(mode),
-                                        _lib.ptr(u), ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset),
-                                        _lib.ptr(q), _lib.ptr(p), _lib.stream_of(y)), "conditional_fwd")
-        ctx.conf = (int(kind), int(mode), mean is not None)
+        _lib.check(L.ic_conditional_fwd_bin(_lib.ptr(y), _lib.ptr(scale), _lib.ptr(mean), _n(y), int(kind),
+                                            int(mode), _lib.ptr(u), ctypes.c_ulonglong(seed),
+                                            ctypes.c_ulonglong(offset), float(bin_), _lib.ptr(q), _lib.ptr(p),
+                                            _lib.stream_of(y)), "conditional_fwd")
+        ctx.conf = (int(kind), int(mode), mean is not None, float(bin_))
         ctx.save_for_backward(q, scale, mean)
         return q, p
 
     @staticmethod
     def backward(ctx, gq, gp):
         q, scale, mean = ctx.saved_tensors
-        kind, mode, has_mean = ctx.conf
+        kind, mode, has_mean, bin_ = ctx.conf
         L = _L()
         gq = None if gq is None else _match(gq, q)
         gp = None if gp is None else _match(gp, q)
         dy = torch.empty_like(q) if ctx.needs_input_grad[0] else None
         ds = torch.empty_like(q) if ctx.needs_input_grad[1] else None
         dm = torch.empty_like(q) if (has_mean and ctx.needs_input_grad[2]) else None
-        _lib.check(L.ic_conditional_bwd(_lib.ptr(q), _lib.ptr(scale), _lib.ptr(mean), _n(q), kind,
-                                        _lib.ptr(gq), _lib.ptr(gp), _lib.ptr(dy), _lib.ptr(ds), _lib.ptr(dm),
-                                        _lib.stream_of(q)), "conditional_bwd")
+        _lib.check(L.ic_conditional_bwd_bin(_lib.ptr(q), _lib.ptr(scale), _lib.ptr(mean), _n(q), kind, bin_,
+                                            _lib.ptr(gq), _lib.ptr(gp), _lib.ptr(dy), _lib.ptr(ds), _lib.ptr(dm),
+                                            _lib.stream_of(q)), "conditional_bwd")
         if mode == 1 and dy is not None:  # round: zero gradient through q
             if gp is None:
                 dy.zero_()
             else:
                 dy.zero_()
-        return dy, ds, dm, None, None, None, None, None
+        return dy, ds, dm, None, None, None, None, None, None
 
 
-def factorized(z, params, train, u=None):
-    """Returns (q, p) for EntropyModel; `u` optional injected U[0,1) draws."""
+def factorized(z, params, train, u=None, dims=(1, 3, 3, 3, 1), bin_=1.0):
+    """Returns (q, p) for EntropyModel; `u` optional injected U[0,1) draws.  The default CDF MLP
+    (DIMS [3, 3, 3]) with BIN 1 runs the fused fixed-width kernels, anything else the generic ones."""
     if not train:
         mode, seed, off = 1, 0, 0
     elif u is not None:
@@ -495,10 +566,12 @@ def factorized(z, params, train, u=None):
     else:
         mode, seed = 3, 0
         u, off = _noise.philox_stream(z.numel(), z.device)
-    return FactorizedFn.apply(z, mode, u, seed, off, *params)
+    if list(dims) == [1, 3, 3, 3, 1] and float(bin_) == 1.0:
+        return FactorizedFn.apply(z, mode, u, seed, off, *params)
+    return FactorizedNetFn.apply(z, mode, u, seed, off, tuple(int(d) for d in dims), float(bin_), *params)
 
 
-def conditional(y, scale, mean, kind, train, u=None):
+def conditional(y, scale, mean, kind, train, u=None, bin_=1.0):
     if not train:
         mode, seed, off = 1, 0, 0
     elif u is not None:
@@ -506,7 +579,7 @@ def conditional(y, scale, mean, kind, train, u=None):
     else:
         mode, seed = 3, 0
         u, off = _noise.philox_stream(y.numel(), y.device)
-    return ConditionalFn.apply(y, scale, mean, kind, mode, u, seed, off)
+    return ConditionalFn.apply(y, scale, mean, kind, mode, u, seed, off, float(bin_))
 
 
 class SqDiffFn(Function):

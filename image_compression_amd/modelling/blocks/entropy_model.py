@@ -4,7 +4,9 @@ EntropyModel (factorized prior on z, :188-269) and the symmetric conditional
 models on y (:272-378).  Noise/round + likelihood run in fused HIP kernels
 (csrc/entropy.hip): the factorized CDF MLP (1->3->3->3->1 per channel, softplus
 weights, tanh gates) is evaluated twice per element in registers, and the
-per-channel parameter gradients are deterministic block reductions.
+per-channel parameter gradients are deterministic block reductions.  Other
+cfg.MODEL.ENTROPY_MODEL.DIMS (up to 5 hidden layers of width <= 8) and any
+BIN run the generic kernels (ic_factorized_*_net, ic_conditional_*_bin).
 """
 import math
 
@@ -106,15 +108,11 @@ class EntropyModel(BaseEntropyModel):
         super().__init__()
         em = cfg.MODEL.ENTROPY_MODEL
         self._cdf_estimator = CDFEstimator(in_channels, em.DIMS, em.INIT_SCALE)
-        if list(self._cdf_estimator.dims) != [1, 3, 3, 3, 1]:
-            raise NotImplementedError("the fused HIP CDF kernel implements DIMS=[3,3,3]")
         self.bin = em.BIN
-        if float(self.bin) != 1.0:
-            raise NotImplementedError("the fused HIP kernels implement BIN=1")
 
     def forward(self, x):
         u = _noise.pop_injected() if self.training else None
-        q, p = factorized(x, self._cdf_estimator.flat_params(), self.training, u)
+        q, p = factorized(x, self._cdf_estimator.flat_params(), self.training, u, self._cdf_estimator.dims, self.bin)
         probs = _ref_layout(p)
         return q, probs, self._ce_loss(probs)
 
@@ -129,8 +127,6 @@ class SymmetricConditionalModel(BaseEntropyModel):
     def __init__(self, cfg):
         super().__init__()
         self.bin = cfg.MODEL.ENTROPY_MODEL.BIN
-        if float(self.bin) != 1.0:
-            raise NotImplementedError("the fused HIP kernels implement BIN=1")
 
     def forward(self, x, scale, mean=0):
         if isinstance(mean, torch.Tensor):
@@ -140,7 +136,7 @@ class SymmetricConditionalModel(BaseEntropyModel):
         else:
             mean_t = torch.full_like(x, float(mean))
         u = _noise.pop_injected() if self.training else None
-        return conditional(x, scale.expand_as(x), mean_t, self.KIND, self.training, u)
+        return conditional(x, scale.expand_as(x), mean_t, self.KIND, self.training, u, self.bin)
 
 
 @ENTROPY_MODEL_REGISTRY.register()

@@ -259,6 +259,31 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
                       const float* dq, const float* dp, float* dz, const ic_fact_grads* grd,
                       void* stream);
 
+/* ---- factorized entropy model, any CDF MLP (cfg.MODEL.ENTROPY_MODEL.DIMS) and BIN
+ *      (modelling/blocks/entropy_model.py:88-99 CDFEstimator, :198 / :229-232 / :259-269 BIN):
+ *      layer l maps dims[l] -> dims[l+1] channels-wise, dims = {1, DIMS..., 1}; per layer
+ *      w[l] [C][dims[l+1]][dims[l]], b[l] [C][dims[l+1]], f[l] [C][dims[l+1]] (NULL on the last
+ *      layer: no gate).  Noise u - bin/2, mass between q -+ bin/2.  Modes as ic_factorized_fwd. */
+#define IC_FACT_MAXL 6   /* layers, len(DIMS) + 1 */
+#define IC_FACT_MAXW 8   /* hidden width */
+typedef struct ic_fact_net {
+  int nlayers;
+  int dims[IC_FACT_MAXL + 1];
+  const float* w[IC_FACT_MAXL];
+  const float* b[IC_FACT_MAXL];
+  const float* f[IC_FACT_MAXL];
+} ic_fact_net;
+typedef struct ic_fact_net_grads {
+  float* w[IC_FACT_MAXL];
+  float* b[IC_FACT_MAXL];
+  float* f[IC_FACT_MAXL];
+} ic_fact_net_grads;
+int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
+                          const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                          void* stream);
+int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
+                          const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream);
+
 /* ---- conditional (Laplacian kind=0 / Gaussian kind=1), mean = 0 or tensor ----
  *      q = y + (u - 0.5) (mode 0), round(y) (mode 1), Philox (mode 2), Philox on the
  *      device state `u` (mode 3, as for ic_factorized_fwd)
@@ -269,6 +294,14 @@ int ic_conditional_fwd(const float* y, const float* scale, const float* mean, lo
 int ic_conditional_bwd(const float* q, const float* scale, const float* mean, long long n, int kind,
                        const float* dq, const float* dp, float* dy, float* dscale, float* dmean,
                        void* stream);
+/* the same with the quantization bin of cfg.MODEL.ENTROPY_MODEL.BIN (the plain entry points: 1):
+ * noise u - bin/2, p = F((bin/2-|q-mean|)/scale) - F((-bin/2-|q-mean|)/scale)
+ * (entropy_model.py:278, :331-334, :343-350) */
+int ic_conditional_fwd_bin(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
+                           const float* u, unsigned long long seed, unsigned long long offset, float bin, float* q,
+                           float* p, void* stream);
+int ic_conditional_bwd_bin(const float* q, const float* scale, const float* mean, long long n, int kind, float bin,
+                           const float* dq, const float* dp, float* dy, float* dscale, float* dmean, void* stream);
 
 /* ---- optimizer: multi-tensor AdamW with fused clip_grad_value_ ----
  * torch.optim.AdamW (solver/optim.py:20-45: per-parameter lr / weight_decay

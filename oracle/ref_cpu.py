@@ -175,7 +175,7 @@ def ce_loss(p):
     return torch.clamp(-1.0 * torch.log(p + 1e-10) / LN2, 0, 50).sum()
 
 
-def cdf_logits(P, x, n_layers=4, prefix="entropy_model._cdf_estimator.layers."):
+def cdf_logits(P, x, n_layers=None, prefix="entropy_model._cdf_estimator.layers."):
     """entropy_model.py:67-78 (CDFLayer) and :101-114 (CDFEstimator): per
     channel c, h <- softplus(W_c) h + b_c, then h <- h + tanh(h) tanh(f_c) on all
     but the last layer. x: (N, C, *).
@@ -186,6 +186,10 @@ def cdf_logits(P, x, n_layers=4, prefix="entropy_model._cdf_estimator.layers."):
     (N, W, C, H) with out[n, w, c, h] = cdf(x)[n, c, h, w].  Only the returned
     probability tensor's layout is affected (the CE sum is permutation
     invariant)."""
+    if n_layers is None:  # len(DIMS) + 1 layers (entropy_model.py:90), as many as P holds
+        n_layers = 0
+        while f"{prefix}{n_layers}.weight" in P:
+            n_layers += 1
     N, C = x.shape[:2]
     sp = x.shape[2:]
     order = [0] + list(range(2, x.dim())) + [1]
@@ -357,16 +361,16 @@ def ms_ssim_metric_db(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
 # ---------------------------------------------------------------- full model
 def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             loss_names=("MSE",), lam=256.0, ssim_log=True,
-            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None):
+            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None, bin_=1.0):
     """modelling/meta_arch/bmshl2018.py:68-98 Compressor2018.forward.
     Returns dict of intermediates and the loss dict."""
     N, C, H, W = x.shape
     num_pixels = N * H * W
     y = analysis(P, x, strides)
     z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl)
-    z_tilde, p_z, ce_z = factorized(P, z, u_z, train)
+    z_tilde, p_z, ce_z = factorized(P, z, u_z, train, bin_)
     sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl)
-    y_tilde, p_y = conditional(y, sigma, u_y, train, cond)
+    y_tilde, p_y = conditional(y, sigma, u_y, train, cond, bin_=bin_)
     ce_y = ce_loss(p_y)
     x_raw = synthesis(P, y_tilde, strides)
     x_tilde = lower_bound(upper_bound(x_raw, 1.0), 0.0)

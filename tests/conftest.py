@@ -40,6 +40,7 @@ def oracle_kwargs(meta):
         loss_names=tuple(over.get("MODEL.LOSS.DISTORTION_LOSS_NAMES", ["MSE"])),
         lam=float(over.get("MODEL.LOSS.DISTORTION_LOSS_WEIGHT", 1.0)),
         ssim_log=bool(over.get("MODEL.LOSS.SSIM.LOG_SCALE", False)),
+        bin_=float(over.get("MODEL.ENTROPY_MODEL.BIN", 1.0)),
     )
 
 

@@ -16,8 +16,9 @@ How the reference is driven (no reference file is modified or copied):
   * forward hooks capture y, z, (z~, p_z, ce_z), sigma, (y~, p_y), and the raw
     synthesis output; `losses["total_loss"].backward()` gives every `.grad`.
 
-Usage:  python tools/gen_golden.py            (writes tests/golden/*.npz)
+Usage:  python tools/gen_golden.py [case ...]   (writes tests/golden/*.npz; all cases by default)
 """
+import copy
 import json
 import os
 import sys
@@ -40,7 +41,9 @@ def _cfg(get_cfg_defaults, over):
         parts = key.split(".")
         for p in parts[:-1]:
             node = node[p]
-        node[parts[-1]] = val
+        # a copy: CDFEstimator inserts the 1-wide ends into cfg DIMS in place
+        # (entropy_model.py:92-93), which must not leak into the recorded `over`
+        node[parts[-1]] = copy.deepcopy(val)
     return cfg
 
 
@@ -154,9 +157,24 @@ def main():
          1, 192, 192, True, 4),
         # non-square, non-power-of-two spatial size (H,W % 64 == 0)
         ("small_laplace_mse_rect_train", dict(SMALL), 1, 64, 128, True, 5),
+        # entropy-model generality: other CDF MLP widths (DIMS) and quantization bins (BIN)
+        ("small_dims242_bin2_laplace_train",
+         dict(SMALL, **{"MODEL.ENTROPY_MODEL.DIMS": [2, 4, 2], "MODEL.ENTROPY_MODEL.BIN": 2.0}),
+         2, 64, 64, True, 6),
+        ("small_dims5_bin05_gauss_train",
+         dict(SMALL, **{"MODEL.ENTROPY_MODEL.DIMS": [5], "MODEL.ENTROPY_MODEL.BIN": 0.5,
+                        "MODEL.ENTROPY_MODEL.CONDITIONAL_MODEL": "GaussianConditionalModel"}),
+         2, 64, 64, True, 7),
+        ("small_dims8x5_bin1_laplace_eval",
+         dict(SMALL, **{"MODEL.ENTROPY_MODEL.DIMS": [8, 8, 8, 8, 8]}), 2, 64, 64, False, 8),
     ]
+    only = set(sys.argv[1:])
     for name, over, N, H, W, train, seed in cases:
+        if only and name not in only:
+            continue
         run_case(modelling, get_cfg_defaults, name, over, N, H, W, train, seed)
+    if only and "full_laplace_mse_train" not in only:
+        return 0
     # full-width default config (192/192, Laplacian, MSE, lambda=256)
     run_case(modelling, get_cfg_defaults, "full_laplace_mse_train",
              {"MODEL.LOSS.DISTORTION_LOSS_WEIGHT": 256.0}, 1, 64, 64, True, 0,
