@@ -131,6 +131,7 @@ SIGNATURES = {
                                        c_void, c_void, c_void]),
     "ic_conditional_bwd_bin": (c_int, [c_void, c_void, c_void, c_ll, c_int, c_float, c_void, c_void, c_void, c_void,
                                        c_void, c_void]),
+    "ic_quantize": (c_int, [c_void, c_ll, c_int, c_void, c_ull, c_ull, c_float, c_void, c_void]),
     "ic_factorized_fwd_net": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_int, c_void, c_ull, c_ull, c_void,
                                       c_void, c_void]),
     "ic_factorized_bwd_net": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_void, c_void, c_void,

@@ -262,7 +262,8 @@ __global__ void cond_fwd_k(const float* y, const float* sc, const float* mean, l
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const long long i = 4 * j + e;
-      if (i < n) cond_elem(y, sc, mean, i, kind, mode == 0 ? u[i] : r[e], mode, half, qo, po);
+      // mode 4: y is already quantized (q = y + 0)
+      if (i < n) cond_elem(y, sc, mean, i, kind, mode == 0 ? u[i] : (mode == 4 ? half : r[e]), mode, half, qo, po);
     }
   }
 }
@@ -530,6 +531,27 @@ __global__ void __launch_bounds__(FNT) fact_bwd_net_k(const float* qin, long lon
   }
 }
 
+// the conditional model's quantization alone (entropy_model.py:331-336), element for
+// element as cond_fwd_k forms it: q = y + (u - bin/2) or round(y)
+__global__ void quant_k(const float* y, long long n, int mode, const float* u, unsigned long long seed,
+                        unsigned long long off, float half, float* qo) {
+  const long long nq = (n + 3) >> 2;
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq; j += (long long)gridDim.x * blockDim.x) {
+    floatx4v r = {0.f, 0.f, 0.f, 0.f};
+    if (mode == 3) {
+      const unsigned long long* st = (const unsigned long long*)u;
+      r = philox_uniform4(st[0], ((st[1] + off) >> 2) + (unsigned long long)j);
+    } else if (mode == 2) {
+      r = philox_uniform4(seed, (off >> 2) + (unsigned long long)j);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * j + e;
+      if (i < n) qo[i] = mode == 1 ? rintf(y[i]) : y[i] + ((mode == 0 ? u[i] : r[e]) - half);
+    }
+  }
+}
+
 bool fact_net_ok(const ic_fact_net* N) {
   if (!N || N->nlayers < 1 || N->nlayers > FML || N->dims[0] != 1 || N->dims[N->nlayers] != 1) return false;
   for (int l = 0; l < N->nlayers; ++l) {
@@ -570,10 +592,23 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
   return IC_OK;
 }
 
+int ic_quantize(const float* y, long long n, int mode, const float* u, unsigned long long seed,
+                unsigned long long offset, float bin, float* q, void* stream) {
+  if ((mode == 0 && !u) || mode < 0 || mode > 3 || !(bin > 0.f)) return IC_ERR_ARG;
+  if (mode == 2 && (offset & 3)) return IC_ERR_ARG;
+  long long b = (n + 1023) / 1024;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(quant_k, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, y, n, mode, u, seed, offset,
+                     0.5f * bin, q);
+  IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+
 int ic_conditional_fwd_bin(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
                            const float* u, unsigned long long seed, unsigned long long offset, float bin, float* q,
                            float* p, void* stream) {
-  if (mode == 0 && !u) return IC_ERR_ARG;
+  if ((mode == 0 && !u) || mode < 0 || mode > 4) return IC_ERR_ARG;
   if (!(bin > 0.f)) return IC_ERR_ARG;
   if (mode == 2 && (offset & 3)) return IC_ERR_ARG;  // stream offsets are whole Philox blocks
   long long b = (n + 1023) / 1024;

@@ -556,6 +556,49 @@ class ConditionalFn(Function):
         return dy, ds, dm, None, None, None, None, None, None
 
 
+class QuantizeFn(Function):
+    """SymmetricConditionalModel._quantize alone (entropy_model.py:319-336): y + (u - bin/2) in
+    training (straight-through: dq/dy = 1), round(y) in evaluation (zero gradient).  The same
+    draws, element for element, as ConditionalFn's quantization (ic_quantize)."""
+
+    @staticmethod
+    def forward(ctx, y, mode, u, seed, offset, bin_):
+        _lib.require_device(y, None if mode == 3 else u)
+        y = _dense(y)
+        if u is not None and mode != 3:
+            u = _match(u.to(y.dtype), y)
+        q = torch.empty_like(y)
+        _lib.check(_L().ic_quantize(_lib.ptr(y), _n(y), int(mode), _lib.ptr(u), ctypes.c_ulonglong(seed),
+                                    ctypes.c_ulonglong(offset), float(bin_), _lib.ptr(q), _lib.stream_of(y)),
+                   "quantize")
+        ctx.mode = int(mode)
+        return q
+
+    @staticmethod
+    def backward(ctx, gq):
+        if ctx.mode == 1:  # torch.round has zero gradient
+            return torch.zeros_like(gq), None, None, None, None, None
+        return gq, None, None, None, None, None
+
+
+def quantize(y, train, u=None, bin_=1.0):
+    """The conditional model's quantization on its own (see conditional_likelihood)."""
+    if not train:
+        mode, seed, off = 1, 0, 0
+    elif u is not None:
+        mode, seed, off = 0, 0, 0
+    else:
+        mode, seed = 3, 0
+        u, off = _noise.philox_stream(y.numel(), y.device)
+    return QuantizeFn.apply(y, mode, u, seed, off, float(bin_))
+
+
+def conditional_likelihood(q, scale, mean, kind, bin_=1.0):
+    """The conditional model's likelihood of already-quantized symbols q (ConditionalFn mode 4:
+    q passes through unchanged, gradients reach q and scale as in the fused op)."""
+    return ConditionalFn.apply(q, scale, mean, kind, 4, None, 0, 0, float(bin_))[1]
+
+
 def factorized(z, params, train, u=None, dims=(1, 3, 3, 3, 1), bin_=1.0):
     """Returns (q, p) for EntropyModel; `u` optional injected U[0,1) draws.  The default CDF MLP
     (DIMS [3, 3, 3]) with BIN 1 runs the fused fixed-width kernels, anything else the generic ones."""

@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import noise as _noise
-from ...functional import CELossFn, conditional, factorized
+from ...functional import CELossFn, conditional, conditional_likelihood, factorized, quantize
 from .build import ENTROPY_MODEL_REGISTRY
 
 LOG2 = math.log(2.0)
@@ -127,6 +127,16 @@ class SymmetricConditionalModel(BaseEntropyModel):
     def __init__(self, cfg):
         super().__init__()
         self.bin = cfg.MODEL.ENTROPY_MODEL.BIN
+
+    def quantize(self, x):
+        """_quantize on its own (train: noise, eval: round): with likelihood() the two halves of
+        forward(), which Compressor2018 runs apart so the hyperprior can run meanwhile."""
+        u = _noise.pop_injected() if self.training else None
+        return quantize(x, self.training, u, self.bin)
+
+    def likelihood(self, q, scale):
+        """_prob_mass of already-quantized q (mean 0)."""
+        return conditional_likelihood(q, scale.expand_as(q), None, self.KIND, self.bin)
 
     def forward(self, x, scale, mean=0):
         if isinstance(mean, torch.Tensor):

@@ -4,6 +4,7 @@ modelling/meta_arch/bmshl2018.py:49-110), every tensor op on HIP kernels.
 forward(x) -> (x_tilde.detach(), losses) with losses =
 {z_entropy, y_entropy, bpp, total_loss, <distortion names>}; only
 total_loss carries grad."""
+import torch
 import torch.nn as nn
 
 from ... import noise as _noise
@@ -13,6 +14,17 @@ from ..blocks import (ENTROPY_MODEL_REGISTRY, AnalysisTransform, HyperpriorAnaly
 from ..layers import LowerBound, UpperBound
 from ..loss import get_loss_dict
 from .build import META_ARCH_REGISTRY
+
+
+_SIDE = {}
+
+
+def _side_stream(device):
+    """One high-priority side stream per device for the hyperprior branch."""
+    k = device.index if device.index is not None else torch.cuda.current_device()
+    if k not in _SIDE:
+        _SIDE[k] = torch.cuda.Stream(device=device, priority=-1)
+    return _SIDE[k]
 
 
 @META_ARCH_REGISTRY.register()
@@ -31,6 +43,9 @@ class Compressor2018(nn.Module):
         self.distortion_loss_fns = get_loss_dict(cfg, cfg.MODEL.LOSS.DISTORTION_LOSS_NAMES)
         self.distortion_loss_weight = cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT
         self.loss_names = ["y_entropy", "z_entropy", "bpp"] + list(self.distortion_loss_fns.keys())
+        # the hyperprior branch (h_a, factorized model, h_s, the y likelihood) on a second
+        # stream, concurrent with the synthesis transform (see forward)
+        self.concurrent_hyperprior = True
 
     def forward(self, x):
         if self.training:
@@ -38,15 +53,46 @@ class Compressor2018(nn.Module):
         N, _, H, W = x.shape
         num_pixels = N * H * W
         y = self.analysis_transform(x)
-        z = self.prior_analysis(AbsFn.apply(y))
-        z_tilde, _z_probs, z_ce = self.entropy_model(z)
-        sigma = self.prior_synthesis(z_tilde)
-        y_tilde, y_probs = self.conditional_model(y, sigma)
-        y_ce = self.conditional_model._ce_loss(y_probs)
-        x_tilde = self.synthesis_transform(y_tilde)
-        x_tilde = LowerBound.apply(UpperBound.apply(x_tilde, 1.), 0.)
-
-        dist = self.distortion_loss(x, x_tilde)
+        cm = self.conditional_model
+        # the split path calls cm.quantize / cm.likelihood instead of cm(y, sigma): with a
+        # forward hook on cm (a caller observing its (q, p)) the call stays whole (serial)
+        hooked = bool(cm._forward_hooks or cm._forward_pre_hooks or nn.modules.module._global_forward_hooks
+                      or nn.modules.module._global_forward_pre_hooks)
+        if self.concurrent_hyperprior and x.is_cuda and hasattr(cm, "quantize") and not hooked:
+            # y~ = y + noise (train) / round(y) (eval) does not depend on sigma, so the synthesis
+            # transform need not wait for the hyperprior: the hyperprior branch and the y
+            # likelihood run on a side stream while g_s runs here, and autograd runs their
+            # backward on the same streams (the small hyperprior kernels hide under g_s's).
+            # Same kernels, same draws in the same order (z, then y): bitwise the serial result.
+            main = torch.cuda.current_stream(x.device)
+            side = _side_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                y.record_stream(side)
+                z = self.prior_analysis(AbsFn.apply(y))
+                z_tilde, _z_probs, z_ce = self.entropy_model(z)
+                sigma = self.prior_synthesis(z_tilde)
+            y_tilde = self.conditional_model.quantize(y)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                y_tilde.record_stream(side)
+                y_probs = self.conditional_model.likelihood(y_tilde, sigma)
+                y_ce = self.conditional_model._ce_loss(y_probs)
+            x_tilde = self.synthesis_transform(y_tilde)
+            x_tilde = LowerBound.apply(UpperBound.apply(x_tilde, 1.), 0.)
+            dist = self.distortion_loss(x, x_tilde)
+            main.wait_stream(side)
+            z_ce.record_stream(main)
+            y_ce.record_stream(main)
+        else:
+            z = self.prior_analysis(AbsFn.apply(y))
+            z_tilde, _z_probs, z_ce = self.entropy_model(z)
+            sigma = self.prior_synthesis(z_tilde)
+            y_tilde, y_probs = self.conditional_model(y, sigma)
+            y_ce = self.conditional_model._ce_loss(y_probs)
+            x_tilde = self.synthesis_transform(y_tilde)
+            x_tilde = LowerBound.apply(UpperBound.apply(x_tilde, 1.), 0.)
+            dist = self.distortion_loss(x, x_tilde)
         total_dist = sum(dist.values())
         entropy = (z_ce + y_ce) / num_pixels
         total = self.distortion_loss_weight * total_dist + entropy

@@ -284,6 +284,11 @@ int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net*
 int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
                           const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream);
 
+/* ---- quantization of the conditional model alone (entropy_model.py:331-336): q = y + (u - bin/2)
+ *      (modes 0 / 2 / 3 as ic_conditional_fwd, the same draws element for element) or round(y) (mode 1) */
+int ic_quantize(const float* y, long long n, int mode, const float* u, unsigned long long seed,
+                unsigned long long offset, float bin, float* q, void* stream);
+
 /* ---- conditional (Laplacian kind=0 / Gaussian kind=1), mean = 0 or tensor ----
  *      q = y + (u - 0.5) (mode 0), round(y) (mode 1), Philox (mode 2), Philox on the
  *      device state `u` (mode 3, as for ic_factorized_fwd)
@@ -297,6 +302,8 @@ int ic_conditional_bwd(const float* q, const float* scale, const float* mean, lo
 /* the same with the quantization bin of cfg.MODEL.ENTROPY_MODEL.BIN (the plain entry points: 1):
  * noise u - bin/2, p = F((bin/2-|q-mean|)/scale) - F((-bin/2-|q-mean|)/scale)
  * (entropy_model.py:278, :331-334, :343-350) */
+/* mode 4 (the _bin entry points): y is already quantized, q = y -- the likelihood half of the model
+ * after ic_quantize (the model runs the hyperprior on a second stream meanwhile) */
 int ic_conditional_fwd_bin(const float* y, const float* scale, const float* mean, long long n, int kind, int mode,
                            const float* u, unsigned long long seed, unsigned long long offset, float bin, float* q,
                            float* p, void* stream);

@@ -65,3 +65,33 @@ def test_graph_replay_draws_fresh_noise_and_is_reproducible():
     noise._st().offset[noise._key(x.device)] = 4 * 192 * 2 * 2 + 4 * 192 * 8 * 8
     b4 = float(eager(x)["bpp"])
     assert abs(b4 - b1) <= 1e-6 * abs(b1)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_concurrent_hyperprior_is_bitwise_serial(train):
+    """Compressor2018 runs the hyperprior branch and the y likelihood on a side stream while
+    the synthesis transform runs (the backward follows the same streams).  Same kernels, same
+    noise counters in the same order: losses, x~ and every gradient bitwise equal to the serial
+    step -- with the in-kernel Philox noise (train) and with rounding (eval)."""
+    from image_compression_amd import noise
+    x = _x()
+    out = {}
+    for conc in (False, True):
+        m = _model(train)
+        m.concurrent_hyperprior = conc
+        state = noise.device_state(x.device)
+        saved = state.clone()
+        for _ in range(2):  # the second step exercises begin_step's advance after a concurrent step
+            state.copy_(saved) if _ == 0 else None
+            m.zero_grad(set_to_none=True)
+            xt, losses = m(x)
+            losses["total_loss"].backward()
+        torch.cuda.synchronize()
+        out[conc] = (xt.clone(), {k: v.clone() for k, v in losses.items()},
+                     {k: p.grad.clone() for k, p in m.named_parameters()})
+        state.copy_(saved)
+    assert torch.equal(out[False][0], out[True][0])
+    for k in out[False][1]:
+        assert torch.equal(out[False][1][k], out[True][1][k]), k
+    for k in out[False][2]:
+        assert torch.equal(out[False][2][k], out[True][2][k]), k
