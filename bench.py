@@ -300,6 +300,10 @@ def main():
     # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
+    if dist:
+        # the hyperprior side stream is measured and tested at one rank; under DDP the gradient
+        # hooks keep the single-stream backward that the multi-rank path was built and tested on
+        model.concurrent_hyperprior = False
     if not args.graph:
         model = D.wrap(model, dev)
 
