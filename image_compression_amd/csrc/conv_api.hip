@@ -208,13 +208,16 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if ((epi == EPI_NONE || epi == EPI_RELU) &&
       tconv_few_ok(x->c, y->c, k, stride, pad, x->sc, x->sw, x->sh, x->sn, x->h, x->w)) {
     // output-row-stationary kernel (edge.hip): no column buffer in HBM
+    const int split = (math & IC_MATH_SPLIT) ? 1 : 0;
     if (need) {
-      plan_report(tconv_few_kind(x->h, x->w, k, pad, y->h), 0, y->c, 1, 0, 0, -1);
+      const int kind = tconv_few_kind(x->h, x->w, k, pad, y->h);
+      // variant 1: the input-row kernel in split arithmetic
+      plan_report(kind, 0, y->c, 1, 0, 0, -1, (kind == IC_KERNEL_TCONV_FEW_ROWS && split && x->c % 32 == 0) ? 1 : 0);
       *need = 0;
       return IC_OK;
     }
     return tconv_few_run(x->data, x->n, x->h, x->w, x->c, W, y->c, k, pad, bias, epi == EPI_RELU, y->data, y->sn,
-                         y->sc, y->sh, y->sw, y->h, y->w, s);
+                         y->sc, y->sh, y->sw, y->h, y->w, s, split);
   }
   if (y->c <= FEW_CH && x->c % 32 == 0 && x->sc == 1)
     return transposed_col2im(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need);

@@ -503,31 +503,65 @@ __global__ void __launch_bounds__(64 * NWV, 2)
 // starts (k - 1) / 2 rows before its run (halo: nothing emitted), and rows
 // outside the image still store zeros, so every emitted row is exact.  Input
 // traffic ~1.1x the tensor (vs ~2.5x for the output-row-stationary kernel).
+#ifndef TF2_SPLIT
+#define TF2_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) on the input-row kernel
+#endif
 constexpr int TF2_RS = 8;  // ring slots: rows 2r - pad - 2 .. 2r - pad + k - 1 in flight
 
-template <int NWV>
+// X3 (IC_MATH_SPLIT, Cin % 32 == 0): fp32 by the exact three-term bf16 split
+// on v_mfma_f32_16x16x32_bf16 (six products per MAC, 3/8 of the fp32 MFMA's
+// cycles): the weights are staged split, as B fragments
+// [ky][s][part][lq][col][8] (8 consecutive channels 32s + 8lq + e of column
+// col per lane: one b128 read per part), and each lane splits its pixel's
+// 8-channel A fragment per 32-channel step from the same row registers.
+template <int NWV, bool X3>
 __global__ void __launch_bounds__(64 * NWV, 1)
     tconv_few2_kernel(const float* __restrict__ x, int N, int Hin, int Win, int Cin, const float* __restrict__ W,
                       int Cout, int k, int pad, const float* __restrict__ bias, int relu, float* __restrict__ y,
                       long long ysn, long long ysc, long long ysh, long long ysw, int Hout, int Wout, int run) {
+  typedef __bf16 tb4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 tb8 __attribute__((ext_vector_type(8)));
   constexpr int WMAX = 16 * NWV;
   constexpr int NT = 64 * NWV;
-  __shared__ __attribute__((aligned(16))) float wl[5 * 12 * 4 * 16 * 4];  // [ky][u][q][col][v], Cin <= 192
+  // fp32: [ky][u][q][col][v] floats; X3: [ky][s][part][lq][col][8] bf16 (the same 90 KB): Cin <= 192
+  __shared__ __attribute__((aligned(16))) float wl[X3 ? 5 * 6 * 3 * 4 * 16 * 4 : 5 * 12 * 4 * 16 * 4];
   __shared__ __attribute__((aligned(16))) float ring[TF2_RS * WMAX * 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int U = Cin >> 4;
+  const int S = Cin >> 5;
   const int ncol = k * Cout;
-  for (int i = tid; i < k * U * 4 * 16 * 4; i += NT) {
-    const int v = i & 3, col = (i >> 2) & 15, q = (i >> 6) & 3, rr = i >> 8;
-    const int u = rr % U, ky = rr / U;
-    const int c = 16 * u + 4 * q + v;
-    float val = 0.f;
-    if (col < ncol) {
-      const int kx = col / Cout, o = col - (col / Cout) * Cout;
-      val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
+  __bf16* const wb = (__bf16*)wl;
+  constexpr int PART = 4 * 16 * 8;  // bf16 per part of one (ky, s) B fragment set
+  if constexpr (X3) {
+    for (int i = tid; i < k * S * 4 * 16 * 8; i += NT) {
+      const int e = i & 7, col = (i >> 3) & 15, q = (i >> 7) & 3, rr = i >> 9;
+      const int sx = rr % S, ky = rr / S;
+      const int c = 32 * sx + 8 * q + e;
+      float val = 0.f;
+      if (col < ncol) {
+        const int kx = col / Cout, o = col - (col / Cout) * Cout;
+        val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
+      }
+      __bf16 hh, mm, ll;
+      split3_bf16(val, hh, mm, ll);
+      const int o0 = (ky * S + sx) * 3 * PART + (q * 16 + col) * 8 + e;
+      wb[o0] = hh;
+      wb[o0 + PART] = mm;
+      wb[o0 + 2 * PART] = ll;
     }
-    wl[i] = val;
+  } else {
+    for (int i = tid; i < k * U * 4 * 16 * 4; i += NT) {
+      const int v = i & 3, col = (i >> 2) & 15, q = (i >> 6) & 3, rr = i >> 8;
+      const int u = rr % U, ky = rr / U;
+      const int c = 16 * u + 4 * q + v;
+      float val = 0.f;
+      if (col < ncol) {
+        const int kx = col / Cout, o = col - (col / Cout) * Cout;
+        val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
+      }
+      wl[i] = val;
+    }
   }
   __syncthreads();
 
@@ -541,12 +575,15 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   const float* xn = x + (size_t)n * Hin * Win * Cin;
 
   floatx4v a0[12], a1[12];
+  // fp32: a[u] = channels 16u + 4lq .. +3; X3: a[2s + h] = channels 32s + 8lq + 4h .. +3
   auto load = [&](int r, floatx4v (&a)[12]) {
     const bool ok = r >= 0 && r < Hin && px < Win;
-    const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? px : 0)) * Cin + 4 * lq;
+    const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? px : 0)) * Cin + (X3 ? 8 : 4) * lq;
 #pragma unroll
-    for (int u = 0; u < 12; ++u)
-      a[u] = (ok && u < U) ? *(const floatx4v*)(xr + 16 * u) : floatx4v{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 12; ++u) {
+      const int off = X3 ? 32 * (u >> 1) + 4 * (u & 1) : 16 * u;
+      a[u] = (ok && u < U) ? *(const floatx4v*)(xr + off) : floatx4v{0.f, 0.f, 0.f, 0.f};
+    }
   };
   // the two rows completed by input row r (emitted from the block's run on)
   auto emit = [&](int r) {
@@ -577,7 +614,33 @@ __global__ void __launch_bounds__(64 * NWV, 1)
     floatx4v acc[5];
 #pragma unroll
     for (int ky = 0; ky < 5; ++ky) acc[ky] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    if (r >= 0 && r < Hin) {
+    if (X3 && r >= 0 && r < Hin) {
+#pragma unroll
+      for (int sx = 0; sx < 6; ++sx) {
+        if (sx < S) {
+          tb4 h0, m0, l0, h1, m1, l1;
+          split3_bf16x4(a[2 * sx], h0, m0, l0);
+          split3_bf16x4(a[2 * sx + 1], h1, m1, l1);
+          const tb8 ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const tb8 am = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const tb8 al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+          for (int ky = 0; ky < 5; ++ky) {
+            if (ky < k) {
+              const __bf16* bp = wb + (ky * S + sx) * 3 * PART + (lq * 16 + li) * 8;
+              const tb8 b0 = *(const tb8*)bp, b1 = *(const tb8*)(bp + PART), b2 = *(const tb8*)(bp + 2 * PART);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b0, acc[ky], 0, 0, 0);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b1, acc[ky], 0, 0, 0);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b2, acc[ky], 0, 0, 0);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b0, acc[ky], 0, 0, 0);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b1, acc[ky], 0, 0, 0);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b0, acc[ky], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    if (!X3 && r >= 0 && r < Hin) {
 #pragma unroll
       for (int u = 0; u < 12; ++u) {
         if (u < U) {
@@ -726,7 +789,7 @@ bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, 
 
 int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float* W, int Cout, int k, int pad,
                   const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
-                  int Hout, int Wout, hipStream_t s) {
+                  int Hout, int Wout, hipStream_t s, int split) {
   if (((uintptr_t)x & 15) || Hout < 1 || Wout < 1) return IC_ERR_ARG;
   if (tconv_few_kind(Hin, Win, k, pad, Hout) == IC_KERNEL_TCONV_FEW_ROWS) {
     // input-row stationary: runs of input rows, about one block per CU
@@ -734,8 +797,12 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
     if (run < 4) run = 4;
     if (run > Hin) run = Hin;
     const long long blocks = (long long)N * ((Hin + run - 1) / run);
-    hipLaunchKernelGGL((tconv_few2_kernel<8>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W, Cout,
-                       k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
+    if (TF2_SPLIT && split && Cin % 32 == 0)
+      hipLaunchKernelGGL((tconv_few2_kernel<8, true>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W,
+                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
+    else
+      hipLaunchKernelGGL((tconv_few2_kernel<8, false>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W,
+                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
     IC_CHECK_LAUNCH();
     return IC_OK;
   }

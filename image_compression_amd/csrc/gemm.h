@@ -168,7 +168,7 @@ bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, 
                   long long xsn, int Hin, int Win);
 int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float* W, int Cout, int k, int pad,
                   const float* bias, int relu, float* y, long long ysn, long long ysc, long long ysh, long long ysw,
-                  int Hout, int Wout, hipStream_t s);
+                  int Hout, int Wout, hipStream_t s, int split = 0);  // split: IC_MATH_SPLIT (input-row kernel)
 // IC_KERNEL_TCONV_FEW_ROWS or IC_KERNEL_TCONV_FEW: which one tconv_few_run launches
 int tconv_few_kind(int Hin, int Win, int k, int pad, int Hout);
 // ic_conv_plan for GDN (gdn.hip): reports through g_plan_sink

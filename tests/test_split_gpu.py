@@ -93,6 +93,34 @@ def test_tconv_split_fwd_dgrad(n, c, h, w, k, s, p, op):
     _check(dws, dwn, wr.grad, "dw")
 
 
+@pytest.mark.parametrize("n,cin,h,w", [
+    (2, 192, 16, 16),                # g_s.6: 192 -> 3-channel image
+    (2, 192, 9, 7),                  # ragged
+    (3, 96, 12, 20),                 # 3 channel steps of 32
+    (2, 80, 8, 8),                   # Cin % 32 != 0: the fp32 input-row kernel
+])
+def test_tconv_few_split(n, cin, h, w):
+    """The input-row-stationary transposed conv to a few-channel image (tconv_few2_kernel) in
+    split arithmetic: the fp32 bar against fp64; dx / dw run the edge kernels (fp32)."""
+    from image_compression_amd import _lib
+    x = _r(n, cin, h, w, seed=12)
+    wt = _r(cin, 3, 5, 5, seed=13, scale=0.05)
+    xr = x.double().requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, None, stride=2, padding=2, output_padding=1)
+    gy = _r(*yr.shape, seed=14)
+    yr.backward(gy.double())
+    ys, dxs, dws = _tconv(x, wt, 2, 2, 1, 2, gy)
+    yn, dxn, dwn = _tconv(x, wt, 2, 2, 1, 0, gy)
+    split = cin % 32 == 0
+    _check(ys, yn, yr.detach(), "y", ran=split)
+    _check(dxs, dxn, xr.grad, "dx", ran=False)
+    _check(dws, dwn, wr.grad, "dw", ran=False)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    p = _lib.plan("conv_transpose2d_fwd", xd, torch.empty(yr.shape, device=DEV), 5, 2, 2, 2)
+    assert (p["kernel"], p["variant"]) == ("tconv_few_rows", 1 if split else 0), p
+
+
 def test_split_extreme_magnitudes():
     """Operands spanning many binades (the split's residuals stay normal fp32/bf16)."""
     x = _r(2, 192, 16, 16, seed=8) * torch.exp(_r(2, 192, 16, 16, seed=9) * 4)
