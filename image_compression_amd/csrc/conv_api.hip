@@ -351,13 +351,13 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
     const size_t slab = edge_wgrad_ws(G->c, Kc, edge_units(G->n, G->h, G->w));
     const size_t cs = (db && !db_from_g) ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
     if (need) {
-      plan_report(IC_KERNEL_EDGE_WGRAD, G->c, Kc, 1, 0, 0, -1);
+      plan_report(IC_KERNEL_EDGE_WGRAD, G->c, Kc, 1, 0, 0, -1, (math & IC_MATH_SPLIT) ? 1 : 0);  // 1: split
       *need = ic_align(slab, 256) + ic_align(cs, 256);
       return IC_OK;
     }
     if (wsb < ic_align(slab, 256) + ic_align(cs, 256)) return IC_ERR_WORKSPACE;
     int rc = edge_wgrad_run(G->data, G->c, X->data, X->sn, X->sc, X->sh, X->sw, X->n, X->c, X->h, X->w, G->h, G->w,
-                            k, stride, pad, dw, db_from_g ? db : nullptr, ws, s);
+                            k, stride, pad, dw, db_from_g ? db : nullptr, ws, s, (math & IC_MATH_SPLIT) ? 1 : 0);
     if (rc) return rc;
     if (db && !db_from_g)
       rc = colsum(bias_src->data, bias_src->sn, bias_src->sc, bias_src->sh, bias_src->sw, bias_src->n, bias_src->c,

@@ -29,6 +29,9 @@
 
 namespace {
 
+#ifndef EW_SPLIT
+#define EW_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in edge_wgrad_kernel
+#endif
 constexpr int SEG = 64;        // output pixels per work unit (one row segment)
 constexpr int KMAX = 100;      // T*C <= 25 taps x 4 channels
 constexpr int PMAX = 4 * 5 * (63 * 2 + 5);  // patch floats: C x k x (63 s + k)
@@ -57,9 +60,10 @@ constexpr int PREG = (PMAX + 255) / 256;
 
 // This thread's patch elements i = tid + 256 q, decomposed once per launch
 // (the divisions by the runtime patch width and kernel size are not redone
-// per unit): ky = -1 marks i >= C*k*PW.
+// per unit) and packed into one register each: (c << 12) | (ky << 9) | j, or
+// -1 for i >= C*k*PW.
 struct EdgePatchMap {
-  int ky[PREG], j[PREG], coff[PREG];
+  int pk[PREG];
 };
 __device__ __forceinline__ void edge_patch_map(const EdgeGeom& g, EdgePatchMap& m, int tid) {
   const int tot = g.C * g.k * g.PW;
@@ -68,9 +72,7 @@ __device__ __forceinline__ void edge_patch_map(const EdgeGeom& g, EdgePatchMap& 
     const int i = tid + 256 * q;
     const int row = i / g.PW, j = i - (i / g.PW) * g.PW;
     const int c = row / g.k, ky = row - (row / g.k) * g.k;
-    m.ky[q] = i < tot ? ky : -1;
-    m.j[q] = j;
-    m.coff[q] = i < tot ? (int)(c * g.sc) : 0;
+    m.pk[q] = i < tot ? (c << 12) | (ky << 9) | j : -1;
   }
 }
 __device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, const EdgePatchMap& m, long long u,
@@ -83,9 +85,10 @@ __device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, const EdgePat
   const float* xb = g.x + n * g.sn;
 #pragma unroll
   for (int q = 0; q < PREG; ++q) {
-    const int iy = iy0 + m.ky[q], ix = ix0 + m.j[q];
-    const bool ok = m.ky[q] >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    pr[q] = ok ? xb[m.coff[q] + (long long)iy * g.sh + ix] : 0.f;
+    const int pk = m.pk[q];
+    const int iy = iy0 + ((pk >> 9) & 7), ix = ix0 + (pk & 511);
+    const bool ok = pk >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    pr[q] = ok ? xb[(long long)(pk >> 12) * g.sc + (long long)iy * g.sh + ix] : 0.f;
   }
 }
 
@@ -215,9 +218,16 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 // G NHWC-dense [N][Ho][Wo][CG] (pixel stride CG), 16-B aligned; CG in {64,128,192}
 // KTMAX = 16-wide k-tiles compiled for (5 covers the 3-channel 5x5 edges plus
 // the ones column: 76 columns)
-template <int CG, int KTMAX>
+// X3 (IC_MATH_SPLIT): fp32 by the exact three-term bf16 split on
+// v_mfma_f32_16x16x32_bf16 (six products per MAC, 3/8 of the fp32 MFMA's cycles):
+// the same LDS reads of G and of the patch as the fp32 loop (k-slot e of lane
+// group lq takes pixel 32 ks + 4e + lq, so one read instruction spans four
+// consecutive, differently swizzled G rows), split in registers.
+template <int CG, int KTMAX, bool X3>
 __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     edge_wgrad_kernel(const EdgeGeom g, const float* __restrict__ G, int Kc, int ones, float* __restrict__ slab) {
+  typedef __bf16 eb4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 eb8 __attribute__((ext_vector_type(8)));
   constexpr int NTW = CG / 64;            // 16-wide g-tiles per wave
   constexpr int CH = CG / 4;              // 16-B chunks per G row
   constexpr int GT = SEG * CG;            // G tile floats
@@ -254,14 +264,18 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     const long long rr = u / g.units_per_row;
     const long long p0 = rr * g.Wo + (long long)seg * SEG;     // first pixel (n*Ho + oy)*Wo + ox0
     const int valid = min(SEG, g.Wo - seg * SEG);
+    // the per-piece offsets are recomputed per unit, not hoisted out of the
+    // unit loop into live registers (the split loop needs them)
+    int t2 = tid;
+    if (X3) asm volatile("" : "+v"(t2));
 #pragma unroll
     for (int q = 0; q < QP; ++q) {
-      const int pos = tid + 256 * q;
+      const int pos = t2 + 256 * q;
       const int row = pos / CH, pc = pos - (pos / CH) * CH;
       const int lc = pc ^ (row & 15);
       const float* src = edge_zero_page;
       if (row < valid) src = G + (size_t)(p0 + row) * CG + lc * 4;
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(img + (pos - lane) * 4), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(img + (pos - (t2 & 63)) * 4), 16, 0, 0);
     }
   };
 
@@ -281,9 +295,55 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     if (un < g.units) edge_patch_load(g, pm, un, pr);
     const float* gs = lds;
     const float* patch = pbase + buf * PB;
+    if constexpr (X3) {
+      auto split8 = [](const float (&v)[8], eb8& h, eb8& m, eb8& l) {
+        eb4 h0, m0, l0, h1, m1, l1;
+        split3_bf16x4(floatx4v{v[0], v[1], v[2], v[3]}, h0, m0, l0);
+        split3_bf16x4(floatx4v{v[4], v[5], v[6], v[7]}, h1, m1, l1);
+        h = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        m = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+        l = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+#pragma unroll 1
+      for (int ks = 0; ks < SEG / 32; ++ks) {
+        eb8 ah[NTW], am[NTW], al[NTW];
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+          const int gc = gbase + 16 * i + li;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int m = 32 * ks + 4 * e + lq;
+            v[e] = gs[m * CG + ((((gc >> 2) ^ (m & 15)) << 2) | (gc & 3))];
+          }
+          split8(v, ah[i], am[i], al[i]);
+        }
+#pragma unroll
+        for (int kt = 0; kt < KTMAX; ++kt) {
+          if (kt < KT) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = patch[koff[kt] + g.stride * (32 * ks + 4 * e + lq)];
+            eb8 bh, bm, bl;
+            split8(v, bh, bm, bl);
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) {
+              floatx4v& c = acc[i][kt];
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one k-tile's operands live at a time
+        }
+      }
+    }
     // k-step s2 of the pixel reduction: pixel m = 4 s2 + lq
 #pragma unroll 4
-    for (int s2 = 0; s2 < SEG / 4; ++s2) {
+    for (int s2 = 0; s2 < (X3 ? 0 : SEG / 4); ++s2) {
       const int m = 4 * s2 + lq;
       float a[NTW];
 #pragma unroll
@@ -742,7 +802,7 @@ long long edge_units(int N, int Ho, int Wo) { return (long long)N * Ho * ((Wo + 
 // dW[g][c][ky][kx] = sum_p G[p][g] X[p*s + tap][c];  db[g] = sum_p G[p][g] when db != NULL
 int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
                    int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,
-                   void* ws, hipStream_t s) {
+                   void* ws, hipStream_t s, int split) {
   EdgeGeom g;
   if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
   const int Kc = g.TC + (db ? 1 : 0);
@@ -750,8 +810,14 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
   const int grid = edge_grid(g.units, k5 ? 2 : 1);
   if (grid < 1) return IC_OK;
   float* slab = (float*)ws;
-#define EDGE_WG(CG_, KT_) \
-  hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_>), dim3(grid), dim3(256), 0, s, g, G, Kc, db ? 1 : 0, slab)
+  const bool x3 = EW_SPLIT && split;
+#define EDGE_WG(CG_, KT_)                                                                                       \
+  do {                                                                                                          \
+    if (x3) hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, true>), dim3(grid), dim3(256), 0, s, g, G, Kc,     \
+                               db ? 1 : 0, slab);                                                               \
+    else hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, false>), dim3(grid), dim3(256), 0, s, g, G, Kc,       \
+                            db ? 1 : 0, slab);                                                                  \
+  } while (0)
   switch (CG) {
     case 192:
       if (k5) EDGE_WG(192, 5); else EDGE_WG(192, 7);

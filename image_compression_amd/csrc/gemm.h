@@ -176,4 +176,4 @@ int gdn_plan(int bwd, const ic_act* x, int math);
 size_t edge_wgrad_ws(int CG, int Kc, long long units);
 int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long long sc, long long sh, long long sw,
                    int N, int C, int H, int W, int Ho, int Wo, int k, int stride, int pad, float* dw, float* db,
-                   void* ws, hipStream_t s);
+                   void* ws, hipStream_t s, int split = 0);  // split: IC_MATH_SPLIT

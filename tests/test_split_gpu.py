@@ -53,6 +53,7 @@ def _check(split, native, ref, name, ran=True):
 @pytest.mark.parametrize("n,cin,cout,h,w,k,s", [
     (2, 192, 192, 32, 32, 5, 2),     # g_a body layer
     (3, 192, 192, 20, 12, 5, 2),     # ragged, several images
+    (2, 3, 192, 40, 72, 5, 2),       # g_a.0 edge: edge_conv / edge_wgrad (split wgrad), ragged unit
     (2, 192, 192, 16, 16, 3, 1),     # h_a.0
     (2, 320, 192, 8, 8, 5, 2),       # latent 320 reduction
     (2, 96, 64, 18, 10, 5, 2),       # Cout 64 tile, Cin % 64 != 0
@@ -68,7 +69,7 @@ def test_conv_split_fwd_dgrad(n, cin, cout, h, w, k, s):
     yr.backward(gy.double())
     ys, dxs, dws = _conv(x, wt, b, s, k // 2, 2, gy)
     yn, dxn, dwn = _conv(x, wt, b, s, k // 2, 0, gy)
-    _check(ys, yn, yr.detach(), "y")
+    _check(ys, yn, yr.detach(), "y", ran=cin % 32 == 0)          # the 3-channel edge_conv runs fp32
     _check(dxs, dxn, xr.grad, "dx")
     _check(dws, dwn, wr.grad, "dw", ran=min(cin, cout) >= 128)   # split wgrad: >= 128 channels per side
 
@@ -115,7 +116,7 @@ def test_tconv_few_split(n, cin, h, w):
     split = cin % 32 == 0
     _check(ys, yn, yr.detach(), "y", ran=split)
     _check(dxs, dxn, xr.grad, "dx", ran=False)
-    _check(dws, dwn, wr.grad, "dw", ran=False)
+    _check(dws, dwn, wr.grad, "dw", ran=cin in (64, 128, 192))  # edge_wgrad in split arithmetic
     xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
     p = _lib.plan("conv_transpose2d_fwd", xd, torch.empty(yr.shape, device=DEV), 5, 2, 2, 2)
     assert (p["kernel"], p["variant"]) == ("tconv_few_rows", 1 if split else 0), p
