@@ -37,15 +37,17 @@ constexpr int FEW_CH = 8;  // image-edge layers (3 channels) go through im2col /
 
 // few input channels: xcol = im2col(x) (K = k*k*C padded to 32), then one 1x1 GEMM
 int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
-                  const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need) {
+                  const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
   const int T = k * k;
   const int Kp = (int)ic_align((size_t)T * x->c, 32);
   if ((epi == EPI_NONE || epi == EPI_RELU) && edge_conv_ok(x->c, k, stride, x->sw, y->sc, y->c, y->sw, y->sh, y->sn)) {
     // patch-gather kernel (edge.hip): no im2col columns in HBM
     const int Npad = ig_npad(y->c);
     const size_t wpb = (size_t)Npad * Kp * 4;
+    const int split = (math & IC_MATH_SPLIT) ? 1 : 0;
     if (need) {
-      plan_report(IC_KERNEL_EDGE_CONV, 64, y->c, 1, 0, 0, -1);
+      // variant 1: split arithmetic (edge_conv_x3_kernel)
+      plan_report(IC_KERNEL_EDGE_CONV, 64, y->c, 1, 0, 0, -1, edge_conv_split(split, T * x->c, y->c) ? 1 : 0);
       *need = ic_align(wpb, 256);
       return IC_OK;
     }
@@ -56,7 +58,7 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
     int rc = pack_weights(W, y->c, x->c, k, 0, 1, T, ky, kx, Npad, Kp, wp, s);
     if (rc) return rc;
     return edge_conv_run(x->data, x->sn, x->sc, x->sh, x->sw, x->n, x->c, x->h, x->w, wp, Kp, bias, k, stride, pad,
-                         y->data, y->sn, y->sc, y->sh, y->sw, y->c, y->h, y->w, epi == EPI_RELU, s);
+                         y->data, y->sn, y->sc, y->sh, y->sw, y->c, y->h, y->w, epi == EPI_RELU, s, split);
   }
   const long long rows = (long long)x->n * y->h * y->w;
   ic_act xc;
@@ -157,7 +159,7 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w)
     return IC_ERR_ARG;
   if (x->c <= FEW_CH && aop == AOP_NONE)
-    return direct_im2col(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need);
+    return direct_im2col(x, W, bias, k, stride, pad, y, epi, ws, wsb, s, need, math);
   IgDesc d = {};
   set_x(d, x);
   set_y(d, y);

@@ -29,6 +29,9 @@
 
 namespace {
 
+#ifndef EC_SPLIT
+#define EC_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in the edge conv (edge_conv_x3_kernel)
+#endif
 #ifndef EW_SPLIT
 #define EW_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in edge_wgrad_kernel
 #endif
@@ -150,6 +153,7 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
+  const float lo = relu ? 0.f : -__builtin_inff();  // epilogue clamp: ReLU or none
   // zero runs after both patch buffers
   for (int i = tid; i < 2 * SEG * 2; i += 256) {
     lds[PSZ + i] = 0.f;
@@ -187,6 +191,9 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
         }
       }
     }
+    // the next patch into the free buffer before the epilogue's global stores
+    // (waiting for its loads then never waits for stores)
+    if (un < g.units) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
     // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li)
     const int seg = (int)(u % g.units_per_row);
     const long long rr = u / g.units_per_row;
@@ -201,15 +208,163 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           floatx4v v = acc[mt][j] + bv[j];
-          if (relu) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-          }
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], lo);  // branch-free ReLU
           *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = v;
         }
       }
     }
-    if (un < g.units) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
+    buf ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------ conv, split
+// IC_MATH_SPLIT: fp32 by the exact three-term bf16 split on
+// v_mfma_f32_16x16x32_bf16 (six products per MAC, 3/8 of the fp32 MFMA's
+// cycles), T*C <= 96 (three 32-wide k-steps).  The weights, split, sit in LDS
+// as A fragments [part][s][n][32] (16-B chunks XOR (n & 3)): 110 KB, so one
+// block of 8 waves per CU; wave w owns channel slice w & 3 and m-tiles
+// 2 (w >> 2), +1 of every unit.  B fragments (8 consecutive k of one pixel)
+// are gathered from the fp32 patch by the per-lane offset table and split in
+// registers.  The patch pipeline (waves 0-3) and the epilogue are edge_conv's.
+constexpr int EC3_S = 3;
+template <int COUT>
+__global__ void __launch_bounds__(512, 1)
+    edge_conv_x3_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
+                        int relu, float* __restrict__ y, long long ys_n, long long ys_h, long long ys_w) {
+  typedef __bf16 eb4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 eb8 __attribute__((ext_vector_type(8)));
+  constexpr int NTW = COUT / 64;
+  constexpr int PLANE = EC3_S * COUT * 32;  // bf16 per part
+  __shared__ __attribute__((aligned(16))) __bf16 wl[3 * PLANE];
+  __shared__ __attribute__((aligned(16))) float lds[2 * (PMAX + 2 * SEG * 2)];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int nbase = (w & 3) * (COUT / 4);
+  const int mt0 = 2 * (w >> 2);
+  const bool stager = w < 4;  // waves 0-3 carry the patch pipeline
+  const int S = (g.TC + 31) / 32;
+  const int PSZ = g.C * g.k * g.PW;
+  const int zero_off = PSZ;
+  const int bufsz = PMAX + 2 * SEG * 2;
+
+  for (int i = tid; i < EC3_S * COUT * 32; i += 512) {
+    const int kk = i & 31, n = (i >> 5) % COUT, sx = (i >> 5) / COUT;
+    const int kq = 32 * sx + kk;
+    const float v = (sx < S && kq < Kp) ? wp[(size_t)n * Kp + kq] : 0.f;
+    __bf16 hh, mm, ll;
+    split3_bf16(v, hh, mm, ll);
+    const int o = (sx * COUT + n) * 32 + (((kk >> 3) ^ (n & 3)) << 3) + (kk & 7);
+    wl[o] = hh;
+    wl[PLANE + o] = mm;
+    wl[2 * PLANE + o] = ll;
+  }
+  int koff[EC3_S][8];
+#pragma unroll
+  for (int sx = 0; sx < EC3_S; ++sx)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) koff[sx][e] = edge_koff(g, 32 * sx + 8 * lq + e, zero_off, zero_off, false);
+  floatx4v bv[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
+  const float lo = relu ? 0.f : -__builtin_inff();  // epilogue clamp: ReLU or none
+  for (int i = tid; i < 2 * SEG * 2; i += 512) {
+    lds[PSZ + i] = 0.f;
+    lds[bufsz + PSZ + i] = 0.f;
+  }
+
+  EdgePatchMap pm;
+  edge_patch_map(g, pm, tid & 255);
+  long long u = blockIdx.x;
+  int buf = 0;
+  float pr[PREG];
+  if (u < g.units && stager) {
+    edge_patch_load(g, pm, u, pr);
+    edge_patch_store(g, pr, lds, tid);
+  }
+  floatx4v ob[2][NTW];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) ob[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  for (; u < g.units; u += gridDim.x) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) asm volatile("" ::"v"(ob[t][j]));  // keeps `ob` apart from `acc`
+    __syncthreads();  // patch `buf` (and the weights) complete; everyone is done with buf^1
+    const long long un = u + gridDim.x;
+    if (un < g.units && stager) edge_patch_load(g, pm, un, pr);
+    const float* patch = lds + buf * bufsz;
+    floatx4v acc[2][NTW];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sx = 0; sx < EC3_S; ++sx) {
+      if (sx < S) {
+        eb8 aw[3][NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int n = nbase + 16 * j + li;
+          const int o = (sx * COUT + n) * 32 + ((lq ^ (n & 3)) << 3);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) aw[q][j] = *(const eb8*)(wl + q * PLANE + o);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int m = 16 * (mt0 + t) + li;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = patch[koff[sx][e] + g.stride * m];
+          eb4 h0, m0, l0, h1, m1, l1;
+          split3_bf16x4(floatx4v{v[0], v[1], v[2], v[3]}, h0, m0, l0);
+          split3_bf16x4(floatx4v{v[4], v[5], v[6], v[7]}, h1, m1, l1);
+          const eb8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const eb8 bm = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const eb8 bl = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) {
+            floatx4v& c = acc[t][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[2][j], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][j], bm, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bl, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][j], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bm, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bh, c, 0, 0, 0);
+          }
+        }
+      }
+    }
+    // the next patch into the free buffer before the epilogue's global stores:
+    // waiting for its loads then never waits for stores (vmcnt counts both)
+    if (un < g.units && stager) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
+    // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li)
+    const int seg = (int)(u % g.units_per_row);
+    const long long rr = u / g.units_per_row;
+    const int oy = (int)(rr % g.Ho);
+    const int n = (int)(rr / g.Ho);
+    const int ox0 = seg * SEG;
+    float* yb = y + n * ys_n + (long long)oy * ys_h + nbase + 4 * lq;
+    // the stored values stay in registers of their own (`ob`, live across the
+    // unit loop): overwriting a store's data registers waits for the store
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ob[t][j][r] = fmaxf(acc[t][j][r] + bv[j][r], lo);  // branch-free ReLU
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ox = ox0 + 16 * (mt0 + t) + li;
+      if (ox < g.Wo) {
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = ob[t][j];
+      }
+    }
     buf ^= 1;
   }
 }
@@ -751,11 +906,27 @@ __global__ void __launch_bounds__(64 * NWV, 1)
 // y (NHWC, channel stride 1) = conv(x few-channel, wp [Cout][Kp] with k = t*C + c)
 int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H, int W,
                   const float* wp, int Kp, const float* bias, int k, int stride, int pad, float* y, long long ys_n,
-                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s) {
+                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s,
+                  int split) {
   EdgeGeom g;
   if (!edge_geom(g, x, sn, sc, sh, sw, N, C, H, W, Ho, Wo, k, stride, pad)) return IC_ERR_ARG;
   // 16-B channel-quad stores
   if (ys_c != 1 || Kp < g.TC || ((uintptr_t)y & 15) || ys_w % 4 || ys_h % 4 || ys_n % 4) return IC_ERR_ARG;
+  if (edge_conv_split(split, g.TC, Cout)) {
+    const int grid1 = edge_grid(g.units, 1);
+    if (grid1 < 1) return IC_OK;
+    if (Cout == 192)
+      hipLaunchKernelGGL(edge_conv_x3_kernel<192>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
+                         ys_h, ys_w);
+    else if (Cout == 128)
+      hipLaunchKernelGGL(edge_conv_x3_kernel<128>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
+                         ys_h, ys_w);
+    else
+      hipLaunchKernelGGL(edge_conv_x3_kernel<64>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
+                         ys_h, ys_w);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   const int grid = edge_grid(g.units, EDGE_CONV_PER_CU);
   if (grid < 1) return IC_OK;
   switch (Cout) {
@@ -776,6 +947,10 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
   }
   IC_CHECK_LAUNCH();
   return IC_OK;
+}
+
+bool edge_conv_split(int split, int TC, int Cout) {
+  return EC_SPLIT && split && TC <= 32 * EC3_S && (Cout == 64 || Cout == 128 || Cout == 192);
 }
 
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,

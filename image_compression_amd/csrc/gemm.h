@@ -158,9 +158,12 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,
                   long long ys_n);
+// the split edge conv runs for these (IC_MATH_SPLIT, T*C <= 96)
+bool edge_conv_split(int split, int TC, int Cout);
 int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long long sw, int N, int C, int H, int W,
                   const float* wp, int Kp, const float* bias, int k, int stride, int pad, float* y, long long ys_n,
-                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s);
+                  long long ys_c, long long ys_h, long long ys_w, int Cout, int Ho, int Wo, int relu, hipStream_t s,
+                  int split = 0);  // split: IC_MATH_SPLIT
 bool edge_wgrad_ok(int C, int k, int stride, long long sw, const float* G, int CG, long long gs_c, long long gs_w,
                    long long gs_h, long long gs_n, int Ho, int Wo);
 long long edge_units(int N, int Ho, int Wo);

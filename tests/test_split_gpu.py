@@ -23,7 +23,9 @@ def _r(*shape, seed, scale=1.0):
 
 def _conv(x, w, b, s, p, math, gy):
     from image_compression_amd import functional as IF
-    xd = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    # NHWC maps; a few-channel image stays NCHW, as the model feeds it (the edge kernels)
+    xd = x.to(DEV)
+    xd = (xd.contiguous(memory_format=torch.channels_last) if x.shape[1] >= 32 else xd).requires_grad_(True)
     wd = w.to(DEV).requires_grad_(True)
     y = IF.conv2d(xd, wd, None if b is None else b.to(DEV), s, p, math=math)
     y.backward(gy.to(DEV))
@@ -69,7 +71,7 @@ def test_conv_split_fwd_dgrad(n, cin, cout, h, w, k, s):
     yr.backward(gy.double())
     ys, dxs, dws = _conv(x, wt, b, s, k // 2, 2, gy)
     yn, dxn, dwn = _conv(x, wt, b, s, k // 2, 0, gy)
-    _check(ys, yn, yr.detach(), "y", ran=cin % 32 == 0)          # the 3-channel edge_conv runs fp32
+    _check(ys, yn, yr.detach(), "y")
     _check(dxs, dxn, xr.grad, "dx")
     _check(dws, dwn, wr.grad, "dw", ran=min(cin, cout) >= 128)   # split wgrad: >= 128 channels per side
 
@@ -102,7 +104,8 @@ def test_tconv_split_fwd_dgrad(n, c, h, w, k, s, p, op):
 ])
 def test_tconv_few_split(n, cin, h, w):
     """The input-row-stationary transposed conv to a few-channel image (tconv_few2_kernel) in
-    split arithmetic: the fp32 bar against fp64; dx / dw run the edge kernels (fp32)."""
+    split arithmetic: the fp32 bar against fp64; dx / dw run the edge kernels (split for 64 / 128 /
+    192 channels)."""
     from image_compression_amd import _lib
     x = _r(n, cin, h, w, seed=12)
     wt = _r(cin, 3, 5, 5, seed=13, scale=0.05)
@@ -115,7 +118,7 @@ def test_tconv_few_split(n, cin, h, w):
     yn, dxn, dwn = _tconv(x, wt, 2, 2, 1, 0, gy)
     split = cin % 32 == 0
     _check(ys, yn, yr.detach(), "y", ran=split)
-    _check(dxs, dxn, xr.grad, "dx", ran=False)
+    _check(dxs, dxn, xr.grad, "dx", ran=cin in (64, 128, 192))  # edge_conv in split arithmetic
     _check(dws, dwn, wr.grad, "dw", ran=cin in (64, 128, 192))  # edge_wgrad in split arithmetic
     xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
     p = _lib.plan("conv_transpose2d_fwd", xd, torch.empty(yr.shape, device=DEV), 5, 2, 2, 2)
