@@ -153,7 +153,6 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
-  const float lo = relu ? 0.f : -__builtin_inff();  // epilogue clamp: ReLU or none
   // zero runs after both patch buffers
   for (int i = tid; i < 2 * SEG * 2; i += 256) {
     lds[PSZ + i] = 0.f;
@@ -209,7 +208,7 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
         for (int j = 0; j < NTW; ++j) {
           floatx4v v = acc[mt][j] + bv[j];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], lo);  // branch-free ReLU
+          for (int r = 0; r < 4; ++r) v[r] = (relu && !(v[r] > 0.f)) ? 0.f : v[r];  // branch-free ReLU
           *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = v;
         }
       }
@@ -269,7 +268,6 @@ __global__ void __launch_bounds__(512, 1)
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
-  const float lo = relu ? 0.f : -__builtin_inff();  // epilogue clamp: ReLU or none
   for (int i = tid; i < 2 * SEG * 2; i += 512) {
     lds[PSZ + i] = 0.f;
     lds[bufsz + PSZ + i] = 0.f;
@@ -356,7 +354,10 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ob[t][j][r] = fmaxf(acc[t][j][r] + bv[j][r], lo);  // branch-free ReLU
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[t][j][r] + bv[j][r];
+          ob[t][j][r] = (relu && !(v > 0.f)) ? 0.f : v;  // branch-free ReLU
+        }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ox = ox0 + 16 * (mt0 + t) + li;

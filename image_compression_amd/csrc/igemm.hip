@@ -71,12 +71,23 @@ __device__ __forceinline__ uint32_t ig_out_offset(const IgDesc& d, const IgPhase
   return img * (uint32_t)d.ys_n + oy * (uint32_t)d.ys_h + ox * (uint32_t)d.ys_w;
 }
 
+// keep every accumulator register live up to here: a store's data register
+// is then never overwritten while the store is pending (which would wait for it)
+template <int TM, int TN>
+__device__ __forceinline__ void ig_hold32(floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+}
+
 // epilogue shared by the fp32 and bf16 kernels.  C/D map of the 32x32 MFMA:
 // col = lane&31, row = (reg&3)+8*(reg>>2)+4*(lane>>5)
 template <int TM, int TN>
 __device__ __forceinline__ void ig_epilogue(const IgDesc& d, const IgPhase& P, floatx16 (&acc)[TM][TN], uint32_t M,
                                             uint32_t m0, int n0, int wm, int wn, int WM, int WN, int r, int h,
                                             int split) {
+  // stores straight from the held accumulators (see ig_epilogue16)
   if (d.ksplit > 1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -91,6 +102,7 @@ __device__ __forceinline__ void ig_epilogue(const IgDesc& d, const IgPhase& P, f
           if (n < d.Cout) prow[n] = acc[i][j][reg];
         }
       }
+    ig_hold32<TM, TN>(acc);
     return;
   }
   const uint32_t ysc = (uint32_t)d.ys_c;
@@ -108,17 +120,24 @@ __device__ __forceinline__ void ig_epilogue(const IgDesc& d, const IgPhase& P, f
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const float v = acc[i][j][reg] + bj[j];
+          acc[i][j][reg] = (relu && !(v > 0.f)) ? 0.f : v;
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const uint32_t m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         if (m >= M) continue;
         float* yo = d.y + ig_out_offset(d, P, m);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float v = acc[i][j][reg] + bj[j];
-          if (relu) v = v > 0.f ? v : 0.f;
-          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 32 + r) * ysc] = v;
-        }
+        for (int j = 0; j < TN; ++j)
+          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 32 + r) * ysc] = acc[i][j][reg];
       }
+    ig_hold32<TM, TN>(acc);
     return;
   }
 #pragma unroll
@@ -445,6 +464,15 @@ __global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
 // every 16-lane group, and the 8/16-lane write groups on distinct dword banks.
 // The 16x16x32 shape runs 7-8 % faster than 32x32x16 at equal cycles per MAC:
 // the chip holds a higher clock (MI355X_MICROARCH.md, DVFS item 7).
+// keep every accumulator register live (and unread-for-reuse) up to here
+template <int TM, int TN>
+__device__ __forceinline__ void ig_hold(floatx4v (&acc)[TM][TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+}
+
 __device__ __forceinline__ int ig_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
 template <int TM, int TN>
@@ -453,6 +481,10 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
                                               int split) {
   // C/D map of the 16x16 MFMA: col = lane & 15, row = 4 * (lane >> 4) + reg
   const int c16 = lane & 15, g = lane >> 4;
+  // Stores go out straight from the accumulators, which stay live to the end
+  // (ig_hold): overwriting a pending store's data register waits for that
+  // store (s_waitcnt vmcnt), which otherwise serialises the epilogue on the
+  // store latency, one store at a time.
   if (d.ksplit > 1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -467,6 +499,7 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
           if (n < d.Cout) prow[n] = acc[i][j][reg];
         }
       }
+    ig_hold<TM, TN>(acc);
     return;
   }
   const uint32_t ysc = (uint32_t)d.ys_c;
@@ -483,17 +516,24 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const float v = acc[i][j][reg] + bj[j];
+          acc[i][j][reg] = (relu && !(v > 0.f)) ? 0.f : v;
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const uint32_t m = m0 + wm * WM + i * 16 + 4 * g + reg;
         if (m >= M) continue;
         float* yo = d.y + ig_out_offset(d, P, m);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float v = acc[i][j][reg] + bj[j];
-          if (relu) v = v > 0.f ? v : 0.f;
-          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 16 + c16) * ysc] = v;
-        }
+        for (int j = 0; j < TN; ++j)
+          if (nok[j]) yo[(uint32_t)(n0 + wn * WN + j * 16 + c16) * ysc] = acc[i][j][reg];
       }
+    ig_hold<TM, TN>(acc);
     return;
   }
 #pragma unroll
