@@ -710,6 +710,215 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 
 
 
+// Two waves per SIMD (WG_X3_DUAL): the split weight gradient with eight
+// waves of 96 x 48 (g x c) tiles on v_mfma_f32_16x16x32_bf16 — 72 accumulator
+// registers per wave instead of 144, so two waves share each SIMD and one
+// hides the other's fragment reads, staging and barrier waits.  32-pixel K
+// steps (one MFMA K), unpadded 192-bf16 rows whose 16-B chunks are XOR-
+// swizzled by 4 on rows with bit 1 set and by 2 on rows with bit 3 set, so
+// the four 4-row groups of a 16-column transposed read (rows 8lq + q) land on
+// distinct banks; 144 KB of LDS for two stages, one block per CU.  Row-fast
+// only (a step stays inside one output row: Wg % 32 == 0).
+#ifndef WG_X3_DUAL
+#define WG_X3_DUAL 1
+#endif
+template <bool XSQ>
+__global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  constexpr int BM = 192, WM = 96, WN = 48, BK = 32;
+  constexpr int TM = WM / 16, TN = WN / 16;  // 6 x 3 tiles of 16 x 16
+  constexpr int PITCH = 192;
+  constexpr int PLANE = BK * PITCH;
+  constexpr int OPER = 3 * PLANE;
+  constexpr int STAGE = 2 * OPER;
+  constexpr int C4 = BM / 4;
+  constexpr int NT = 512;
+  constexpr int QP = BK * C4 / NT;  // 3 float4 per thread per operand
+  static_assert(QP * NT == BK * C4 && 2 * QP == TM, "one staged slot per two row tiles");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+
+  const int tiles = d.mtiles * d.ntiles;
+  const int nblk = tiles * d.T * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int per_split = tiles * d.T;
+  const int split = wid / per_split;
+  const int bx = wid - split * per_split;
+  const int t = bx / tiles;
+  const int rem = bx - t * tiles;
+  const int mt = rem / d.ntiles, nt = rem - (rem / d.ntiles) * d.ntiles;
+  const int g0 = mt * BM, c0 = nt * BM;
+  const int pb = split * d.pps;
+  int pe = pb + d.pps;
+  if (pe > (int)d.P) pe = (int)d.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dyt = d.dy[t], dxt = d.dx[t];
+
+  auto swz = [](int row) { return ((((row >> 1) & 1) << 5) | (((row >> 3) & 1) << 4)); };
+  int srow[QP], scol[QP];
+#pragma unroll
+  for (int q = 0; q < QP; ++q) {
+    const int f = tid + NT * q;
+    srow[q] = f / C4;
+    scol[q] = (f - (f / C4) * C4) * 4;
+  }
+  floatx4v g0r[QP], x0r[QP], g1r[QP], x1r[QP];
+  struct RowBase {
+    const float* gb;
+    const float* xb;
+    int ix0;
+    bool rowok, live;
+  };
+  auto row_base = [&](int p0, bool live) {
+    const uint32_t img = fdiv((uint32_t)p0, d.fd_hw);
+    const uint32_t rr = (uint32_t)p0 - img * d.fd_hw.d;
+    const uint32_t gy = fdiv(rr, d.fd_w);
+    const uint32_t gx0 = rr - gy * d.fd_w.d;
+    const int iy = (int)gy * d.stride + dyt;
+    return RowBase{d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w,
+                   d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h, (int)gx0 * d.stride + dxt,
+                   live && (unsigned)iy < (unsigned)d.Hx, live};
+  };
+  // branch-free: padding and out-of-range columns read a zero page
+  auto gload_q = [&](const RowBase& rb, int q, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    const int gcol = g0 + scol[q], xcol = c0 + scol[q];
+    const int ix = rb.ix0 + srow[q] * d.stride;
+    const float* gs = (rb.live && gcol < d.Cg) ? rb.gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
+    const float* xs = (rb.rowok && xcol < d.Cx && (unsigned)ix < (unsigned)d.Wx)
+                          ? rb.xb + (long long)ix * d.xs_w + xcol : wg_zero_page;
+    rg[q] = *(const floatx4v*)gs;
+    floatx4v vx = *(const floatx4v*)xs;
+    if (XSQ) vx = vx * vx;
+    rx[q] = vx;
+  };
+  auto gload = [&](int p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP], bool live) {
+    const RowBase rb = row_base(p0, live);
+#pragma unroll
+    for (int q = 0; q < QP; ++q) gload_q(rb, q, rg, rx);
+  };
+  auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
+    __bf16* base = lds + buf * STAGE;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      b4 vh, vm, vl;
+      split3_bf16x4(op == 0 ? rg[q] : rx[q], vh, vm, vl);
+      __bf16* dst = base + op * OPER + srow[q] * PITCH + (scol[q] ^ swz(srow[q]));
+      *(b4*)dst = vh;
+      *(b4*)(dst + PLANE) = vm;
+      *(b4*)(dst + 2 * PLANE) = vl;
+    }
+  };
+  auto sstore = [&](int buf, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
+#pragma unroll
+    for (int q = 0; q < QP; ++q) sstore_q(buf, q, rg, rx);
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  const int li = lane & 15, lq = lane >> 4;
+  // 16x16x32 operands: lane (li, lq) holds pixels 8lq .. 8lq+7 of channel li of its
+  // tile; a transposed read gives a 16-lane group rows 8lq + (li >> 2) (+4), columns 4 (li & 3)
+  const int tr_r = 8 * lq + (li >> 2);
+  const int tr_off = tr_r * PITCH;
+  const int tr_c = 4 * (li & 3);
+  const int tr_sw = swz(tr_r);  // rows tr_r and tr_r + 4 share bits 1 and 3
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](int p0, int buf, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    const __bf16* sb = lds + buf * STAGE;
+    auto tr8 = [&](const __bf16* plane, int col) {
+      const __bf16* src = plane + tr_off + ((col + tr_c) ^ tr_sw);
+      const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)src);
+      const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * PITCH));
+      return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    b8 bb[3][TN];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE, wn * WN + 16 * j);
+    const int pn = p0 + 3 * BK;
+    const RowBase nb = row_base(pn, pn < pe);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      b8 a[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE, wm * WM + 16 * i);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        floatx4v& c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bb[0][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[1][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[2][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[0][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[1][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
+      }
+      if (i & 1) {
+        // the next step's split + store of slot i / 2, then its refill three steps ahead
+        sstore_q(buf ^ 1, i >> 1, rg, rx);
+        gload_q(nb, i >> 1, rg, rx);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);   // MFMA (this and the previous row tile)
+          __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);   // VALU
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
+          if (k == 2 || k == 5) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  // steps run in pairs (two register sets alternate statically); an odd count
+  // is padded with one all-zero step in front
+  const int nsteps = pe > pb ? (pe - pb) / BK : 0;
+  const int q0 = pb - ((nsteps & 1) ? BK : 0);
+  if (nsteps > 0) {
+    if (nsteps & 1) {
+#pragma unroll
+      for (int q = 0; q < QP; ++q) {
+        g0r[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+        x0r[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      gload(q0, g0r, x0r, true);
+    }
+    sstore(0, g0r, x0r);
+    gload(q0 + BK, g1r, x1r, q0 + BK < pe);
+    gload(q0 + 2 * BK, g0r, x0r, q0 + 2 * BK < pe);
+  }
+  __syncthreads();
+  for (int p0 = q0; p0 < pe; p0 += 2 * BK) {
+    step(p0, 0, g1r, x1r);
+    step(p0 + BK, 1, g0r, x0r);
+  }
+
+  // C/D map of the 16x16 MFMA: row (g) = 4 lq + r, col (c) = li
+  float* slab = d.partial + ((long long)split * d.T + t) * (long long)d.Cg * d.ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = g0 + wm * WM + 16 * i + 4 * lq + r;
+      if (gr >= d.Cg) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = c0 + wn * WN + 16 * j + li;
+        if (col < d.ncols) slab[(long long)gr * d.ncols + col] = acc[i][j][r];
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));  // stores straight from held registers
+}
+
 struct WgRed {
   const float* partial;
   float* out;    // final [g][c][kk] (G == 1) or level-2 partial [G][g][t][c]
@@ -789,7 +998,10 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   const bool sq = d.x_op == AOP_SQUARE;
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
-  if (d.rowfast) {
+  if (WG_X3_DUAL && d.rowfast && d.Wg % 32 == 0 && d.pps % 32 == 0) {
+    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true>), grid, dim3(512), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3d_kernel<false>), grid, dim3(512), 0, s, d);
+  } else if (d.rowfast) {
     if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true, TWO>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((wg_x3_kernel<true, false, TWO>), grid, dim3(256), 0, s, d);
   } else {
