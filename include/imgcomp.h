@@ -174,7 +174,8 @@ int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const flo
 #define IC_KERNEL_WG_FP32 11        /* wg_kernel: weight gradient on the fp32 MFMA */
 #define IC_KERNEL_WG_FP32_GATHER 12 /* wg_kernel, flattened (tap, channel) columns */
 #define IC_KERNEL_WG_LDSDMA 13      /* wg_glds_kernel: fp32 MFMA, LDS-DMA staged */
-#define IC_KERNEL_WG_SPLIT 14       /* wg_x3_kernel: weight gradient in split arithmetic */
+#define IC_KERNEL_WG_SPLIT 14       /* wg_x3d_kernel (two waves per SIMD, maps >= 32 wide) / wg_x3_kernel:
+                                       weight gradient in split arithmetic */
 #define IC_KERNEL_EDGE_WGRAD 15     /* edge_wgrad_kernel */
 #define IC_KERNEL_GDN_FUSED 16      /* gdn_fwd_fused_kernel / gdn_bwd_fused_kernel (fp32 dx) */
 #define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3_kernel / gdn_bwd_fused_kernel with split dgamma */
@@ -185,7 +186,8 @@ typedef struct ic_plan {
   int ksplit;        /* implicit GEMM K splits (1 = none; > 1 adds a deterministic partial-sum pass) */
   int nsplit;        /* weight gradient pixel splits (0 for other ops) */
   int im2col;        /* 1 when a column buffer is materialised in HBM */
-  int variant;       /* kernel-specific template variant (weight gradient: 1 = row-fast addressing) */
+  int variant;       /* kernel-specific template variant (weight gradient: 1 = row-fast addressing;
+                        edge conv, edge weight gradient, input-row transposed conv: 1 = split arithmetic) */
   long long blocks;  /* workgroups of the main launch (-1 when not reported) */
 } ic_plan;
 int ic_conv_plan(int op, const ic_act* a, const ic_act* b, int k, int stride, int pad, int math, ic_plan* out);
