@@ -722,7 +722,12 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #ifndef WG_X3_DUAL
 #define WG_X3_DUAL 1
 #endif
-template <bool XSQ>
+#ifndef WG_X3_DUAL16
+#define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
+#endif
+// SEG16: maps 16 wide — a 32-pixel step spans two output rows, each 16-pixel half
+// with its own row base (either half stays inside one row when Wg % 16 == 0)
+template <bool XSQ, bool SEG16>
 __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
@@ -781,11 +786,23 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
                    d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h, (int)gx0 * d.stride + dxt,
                    live && (unsigned)iy < (unsigned)d.Hx, live};
   };
+  struct StepBase {
+    RowBase lo, hi;  // pixels 0..15 and 16..31 of the step (SEG16), else lo only
+  };
+  auto step_base = [&](int p0, bool live) {
+    StepBase sbs;
+    sbs.lo = row_base(p0, live);
+    if constexpr (SEG16) sbs.hi = row_base(p0 + 16, live);
+    return sbs;
+  };
   // branch-free: padding and out-of-range columns read a zero page
-  auto gload_q = [&](const RowBase& rb, int q, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+  auto gload_q = [&](const StepBase& sbs, int q, floatx4v (&rg)[QP], floatx4v (&rx)[QP]) {
+    const bool upper = SEG16 && srow[q] >= 16;
+    const RowBase& rb = upper ? sbs.hi : sbs.lo;
+    const int sr = upper ? srow[q] - 16 : srow[q];
     const int gcol = g0 + scol[q], xcol = c0 + scol[q];
-    const int ix = rb.ix0 + srow[q] * d.stride;
-    const float* gs = (rb.live && gcol < d.Cg) ? rb.gb + (long long)srow[q] * d.gs_w + gcol : wg_zero_page;
+    const int ix = rb.ix0 + sr * d.stride;
+    const float* gs = (rb.live && gcol < d.Cg) ? rb.gb + (long long)sr * d.gs_w + gcol : wg_zero_page;
     const float* xs = (rb.rowok && xcol < d.Cx && (unsigned)ix < (unsigned)d.Wx)
                           ? rb.xb + (long long)ix * d.xs_w + xcol : wg_zero_page;
     rg[q] = *(const floatx4v*)gs;
@@ -794,9 +811,9 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
     rx[q] = vx;
   };
   auto gload = [&](int p0, floatx4v (&rg)[QP], floatx4v (&rx)[QP], bool live) {
-    const RowBase rb = row_base(p0, live);
+    const StepBase sbs = step_base(p0, live);
 #pragma unroll
-    for (int q = 0; q < QP; ++q) gload_q(rb, q, rg, rx);
+    for (int q = 0; q < QP; ++q) gload_q(sbs, q, rg, rx);
   };
   auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QP], const floatx4v (&rx)[QP]) {
     __bf16* base = lds + buf * STAGE;
@@ -843,7 +860,7 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE, wn * WN + 16 * j);
     const int pn = p0 + 3 * BK;
-    const RowBase nb = row_base(pn, pn < pe);
+    const StepBase nb = step_base(pn, pn < pe);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       b8 a[3];
@@ -999,8 +1016,11 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
   if (WG_X3_DUAL && d.rowfast && d.Wg % 32 == 0 && d.pps % 32 == 0) {
-    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true>), grid, dim3(512), 0, s, d);
-    else hipLaunchKernelGGL((wg_x3d_kernel<false>), grid, dim3(512), 0, s, d);
+    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false>), grid, dim3(512), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3d_kernel<false, false>), grid, dim3(512), 0, s, d);
+  } else if (WG_X3_DUAL16 && d.rowfast && d.Wg % 16 == 0 && d.pps % 32 == 0) {
+    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, true>), grid, dim3(512), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3d_kernel<false, true>), grid, dim3(512), 0, s, d);
   } else if (d.rowfast) {
     if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true, TWO>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((wg_x3_kernel<true, false, TWO>), grid, dim3(256), 0, s, d);
