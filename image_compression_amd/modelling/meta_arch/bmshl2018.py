@@ -19,6 +19,23 @@ from .build import META_ARCH_REGISTRY
 _SIDE = {}
 
 
+class _StreamEdge(torch.autograd.Function):
+    """Identity at a stream crossing.  Forward runs on the consumer stream of the value;
+    backward (on that same stream) records the incoming gradient on `other`, the stream
+    that consumes the gradient next, before handing it over."""
+
+    @staticmethod
+    def forward(ctx, t, other):
+        ctx.other = other
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g.record_stream(ctx.other)
+        return g, None
+
+
 def _side_stream(device):
     """One high-priority side stream per device for the hyperprior branch."""
     k = device.index if device.index is not None else torch.cuda.current_device()
@@ -59,6 +76,10 @@ class Compressor2018(nn.Module):
         hooked = bool(cm._forward_hooks or cm._forward_pre_hooks or nn.modules.module._global_forward_hooks
                       or nn.modules.module._global_forward_pre_hooks)
         if self.concurrent_hyperprior and x.is_cuda and hasattr(cm, "quantize") and not hooked:
+            # every tensor that crosses streams passes a _StreamEdge: its gradient, computed on
+            # one stream and consumed on the other, is recorded on the consumer's stream, so the
+            # caching allocator does not hand its memory to the producer stream's next
+            # allocation while the consumer still reads it
             # y~ = y + noise (train) / round(y) (eval) does not depend on sigma, so the synthesis
             # transform need not wait for the hyperprior: the hyperprior branch and the y
             # likelihood run on a side stream while g_s runs here, and autograd runs their
@@ -69,14 +90,15 @@ class Compressor2018(nn.Module):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 y.record_stream(side)
-                z = self.prior_analysis(AbsFn.apply(y))
+                y_s = _StreamEdge.apply(y, main)
+                z = self.prior_analysis(AbsFn.apply(y_s))
                 z_tilde, _z_probs, z_ce = self.entropy_model(z)
                 sigma = self.prior_synthesis(z_tilde)
             y_tilde = self.conditional_model.quantize(y)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 y_tilde.record_stream(side)
-                y_probs = self.conditional_model.likelihood(y_tilde, sigma)
+                y_probs = self.conditional_model.likelihood(_StreamEdge.apply(y_tilde, main), sigma)
                 y_ce = self.conditional_model._ce_loss(y_probs)
             x_tilde = self.synthesis_transform(y_tilde)
             x_tilde = LowerBound.apply(UpperBound.apply(x_tilde, 1.), 0.)
@@ -84,6 +106,8 @@ class Compressor2018(nn.Module):
             main.wait_stream(side)
             z_ce.record_stream(main)
             y_ce.record_stream(main)
+            z_ce = _StreamEdge.apply(z_ce, side)
+            y_ce = _StreamEdge.apply(y_ce, side)
         else:
             z = self.prior_analysis(AbsFn.apply(y))
             z_tilde, _z_probs, z_ce = self.entropy_model(z)

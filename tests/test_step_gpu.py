@@ -95,3 +95,35 @@ def test_concurrent_hyperprior_is_bitwise_serial(train):
         assert torch.equal(out[False][1][k], out[True][1][k]), k
     for k in out[False][2]:
         assert torch.equal(out[False][2][k], out[True][2][k]), k
+
+
+def test_concurrent_step_repeatable_at_c2():
+    """The C2 step (32 x 256^2, fp32_split, injected noise) with the hyperprior side stream,
+    repeated: every gradient bitwise equal run to run and to the serial step.  Guards the
+    stream crossings (bmshl2018._StreamEdge): without the gradients recorded on their
+    consumer stream the caching allocator handed a gradient's memory to the other stream's
+    next allocation while it was still read, and about one step in five came out with a
+    changed CDF-estimator weight gradient element (tools/determinism_probe.py)."""
+    from image_compression_amd import get_cfg_defaults, injected_noise, modelling
+    cfg = get_cfg_defaults()
+    cfg.MODEL.LOSS.REDUCTION = "mean"
+    cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT = 256.0
+    cfg.MODEL.COMPUTE_DTYPE = "fp32_split"
+    torch.manual_seed(0)
+    m = modelling.build_model(cfg).to(DEV).train()
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(32, 3, 256, 256, generator=g).to(DEV)
+    uz = torch.rand(32, 192, 4, 4, generator=g).to(DEV)
+    uy = torch.rand(32, 192, 16, 16, generator=g).to(DEV)
+    runs = []
+    for conc in [False] + [True] * 8:
+        m.concurrent_hyperprior = conc
+        m.zero_grad(set_to_none=True)
+        with injected_noise([uz, uy]):
+            _, losses = m(x)
+            losses["total_loss"].backward()
+        torch.cuda.synchronize()
+        runs.append({k: p.grad.clone() for k, p in m.named_parameters()})
+    for i, r in enumerate(runs[1:], 1):
+        for k, v in r.items():
+            assert torch.equal(v, runs[0][k]), (i, k)
