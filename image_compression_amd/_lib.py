@@ -100,6 +100,8 @@ SIGNATURES = {
     "ic_gdn_fwd_ex": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_int, c_void, c_size, c_void]),
     "ic_gdn_bwd_ex": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_int, c_void, c_size,
                               c_void]),
+    "ic_gdn_bwd_sum_ex": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_int, c_void, c_size,
+                                  c_void]),
     "ic_nonneg_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void]),
     "ic_nonneg_bwd": (c_int, [c_void, c_void, c_ll, c_float, c_void, c_void]),
     "ic_bound_fwd": (c_int, [c_void, c_ll, c_float, c_int, c_void, c_void]),

@@ -95,7 +95,7 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
 
 int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
-                 size_t* need, int math = 0) {
+                 size_t* need, int math = 0, float* dxsum = nullptr) {
   const long long n = act_numel(x);
   const long long P = (long long)x->n * x->h * x->w;
   // fused path: x, dx, norm, dy all NHWC-dense with x's strides; its workspace
@@ -105,7 +105,7 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
       wsb >= fused_ws)
     return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s,
-                         (math & IC_MATH_SPLIT) ? ((math & IC_MATH_GDN_BWD_FULL_SPLIT) ? 2 : 1) : 0);
+                         (math & IC_MATH_SPLIT) ? ((math & IC_MATH_GDN_BWD_FULL_SPLIT) ? 2 : 1) : 0, dxsum);
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};
@@ -158,6 +158,10 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
   }
   if (dbeta) {
     rc = colsum(q, x->sn, x->sc, x->sh, x->sw, x->n, x->c, x->h, x->w, dbeta, 1.f, csw, s);
+    if (rc) return rc;
+  }
+  if (dxsum) {
+    rc = colsum(dx->data, dx->sn, dx->sc, dx->sh, dx->sw, dx->n, dx->c, dx->h, dx->w, dxsum, 1.f, csw, s);
     if (rc) return rc;
   }
   return IC_OK;
@@ -228,6 +232,12 @@ int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const flo
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream) {
   return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,
                       math);
+}
+int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, int math, void* ws,
+                      size_t ws_bytes, void* stream) {
+  return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,
+                      math, dxsum);
 }
 
 }  // extern "C"

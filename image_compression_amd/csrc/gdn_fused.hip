@@ -34,6 +34,9 @@
 #define GDN_SPLIT_PK 1  // split staging through split3_bf16x4 (paired conversions)
 #endif
 
+// per-block backward partials: dgamma (C x C), dbeta (C), column sums of dx (C)
+#define GDN_SLAB(C) ((C) * (C) + 2 * (C))
+
 namespace {
 
 __device__ __attribute__((aligned(16))) float gdn_zero_page[4];
@@ -546,7 +549,7 @@ __global__ void __launch_bounds__(512, 2)
       for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    float db = 0.f;
+    float db = 0.f, dxs = 0.f;
     const int t = tid - 256;
     int buf = 0;
     int it = 0;
@@ -588,9 +591,14 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
       GDN_MARK(it, 5);
+      if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
+        const float* gsd = xs + 2 * TILE;
+        const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
+        for (int m = 0; m < rows; ++m) dxs += gsd[swz<C>(m, t)];
+      }
       buf ^= 1;
     }
-    float* out = slab + (size_t)blockIdx.x * (C * C + C);
+    float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -600,7 +608,10 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
         for (int j = 0; j < 3; ++j) out[(size_t)n * C + 96 * wn2 + 32 * j + r] = acc[i][j][reg];
       }
-    if (t < C) out[C * C + t] = db;
+    if (t < C) {
+      out[C * C + t] = db;
+      out[C * C + C + t] = dxs;
+    }
   } else {
     // ---------------- group B: dgamma[n][k] += sum_m q[m][n] x[m][k]^2, rows n = wbase + 16i + li
     floatx4v dg[NTW][KT];
@@ -608,7 +619,7 @@ __global__ void __launch_bounds__(512, 2)
     for (int i = 0; i < NTW; ++i)
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) dg[i][kt] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    float db = 0.f;  // dbeta[t] partial, t = tid - 256 < C
+    float db = 0.f, dxs = 0.f;  // dbeta[t] and dx column-sum partials, t = tid - 256 < C
     const int t = tid - 256;
     int buf = 0;
     int it = 0;
@@ -665,10 +676,15 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
       GDN_MARK(it, 5);
+      if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
+        const float* gsd = xs + 2 * TILE;
+        const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
+        for (int m = 0; m < rows; ++m) dxs += gsd[swz<C>(m, t)];
+      }
       buf ^= 1;
     }
-    // partials: slab[block][n][k] (C*C) then dbeta [C]
-    float* out = slab + (size_t)blockIdx.x * (C * C + C);
+    // partials: slab[block][n][k] (C*C), dbeta [C], dx column sums [C]
+    float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
 #pragma unroll
     for (int i = 0; i < NTW; ++i)
 #pragma unroll
@@ -680,7 +696,10 @@ __global__ void __launch_bounds__(512, 2)
           const int k = 16 * kt + li;
           out[(size_t)n * C + k] = dg[i][kt][r];
         }
-    if (t < C) out[C * C + t] = db;
+    if (t < C) {
+      out[C * C + t] = db;
+      out[C * C + C + t] = dxs;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -737,6 +756,7 @@ __global__ void __launch_bounds__(768, 1)
 #pragma unroll
     for (int e = 0; e < 16; ++e) dg[t][e] = 0.f;
   floatx4v dbp = {0.f, 0.f, 0.f, 0.f};
+  float dxs = 0.f;  // dx column-sum partial of column tid < C
   // phase-A element of this thread: row pm, logical channel quad plc
   const int pm = tid / (C / 4), ppc = tid - pm * (C / 4), plc = ppc ^ (pm & 15);
   const int a_st = pm * C + 8 * ((plc >> 1) ^ gdn_bsw(pm)) + 4 * (plc & 1);
@@ -859,11 +879,16 @@ __global__ void __launch_bounds__(768, 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // B3
     store_tile<C, BM, NT>(dx, tile * BM, P, gs, tid);
+    if (tid < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
+      const int rows = (P - tile * BM) < (uint32_t)BM ? (int)(P - tile * BM) : BM;
+      for (int m = 0; m < rows; ++m) dxs += gs[swz<C>(m, tid)];
+    }
     buf ^= 1;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  // partials: slab[block][n][k] then dbeta [C]; dbeta's 16 row partials combine in LDS in a fixed order
-  float* out = slab + (size_t)blockIdx.x * (C * C + C);
+  // partials: slab[block][n][k], dbeta [C] (its 16 row partials combine in LDS in a fixed order), dx column sums
+  float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
+  if (tid < C) out[C * C + C + tid] = dxs;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int T = 3 * w + t, ti = T / 6, tj = T - (T / 6) * 6;
@@ -888,9 +913,10 @@ __global__ void __launch_bounds__(768, 1)
 // the partials with eight loads in flight, the quarters combine in LDS in a
 // fixed order
 __global__ void __launch_bounds__(256) gdn_slab_reduce_kernel(const float* __restrict__ slab, int nb, int C,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ dxsum) {
   __shared__ float part[4][64];
-  const int stride = C * C + C;
+  const int stride = GDN_SLAB(C);
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + e;
   const int q = (nb + 3) >> 2, b0 = grp * q, b1 = min(nb, b0 + q);
@@ -910,8 +936,10 @@ __global__ void __launch_bounds__(256) gdn_slab_reduce_kernel(const float* __res
     const float v = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
     if (i < C * C) {
       if (dgamma) dgamma[i] = v;
-    } else if (dbeta) {
-      dbeta[i - C * C] = v;
+    } else if (i < C * C + C) {
+      if (dbeta) dbeta[i - C * C] = v;
+    } else if (dxsum) {
+      dxsum[i - C * C - C] = v;
     }
   }
 }
@@ -937,15 +965,16 @@ int bwd_grid(long long P) {
 
 template <int C, bool X3 = false>
 int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
-                         float* dx, float* dgamma, float* dbeta, long long P, float* slab, hipStream_t s) {
+                         float* dx, float* dgamma, float* dbeta, float* dxsum, long long P, float* slab,
+                         hipStream_t s) {
   const int grid = bwd_grid(P);
   if (grid < 1) return IC_OK;
   hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx,
                      slab, (uint32_t)P);
   IC_CHECK_LAUNCH();
-  const int stride = C * C + C;
+  const int stride = GDN_SLAB(C);
   hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
-                     dbeta);
+                     dbeta, dxsum);
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
@@ -981,10 +1010,10 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
   }
 }
 
-size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * (C * C + C) * sizeof(float); }
+size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * GDN_SLAB(C) * sizeof(float); }
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
-                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split) {
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {
   float* slab = (float*)ws;
   if (split == 2 && C == 192) {
     // whole backward in split arithmetic, one 12-wave block per CU
@@ -993,18 +1022,18 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
     hipLaunchKernelGGL((gdn_bwd_x3_kernel<192>), dim3(grid), dim3(768), 0, s, x, norm, dy, gamma, inverse, dx, slab,
                        (uint32_t)P);
     IC_CHECK_LAUNCH();
-    const int stride = C * C + C;
+    const int stride = GDN_SLAB(C);
     hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
-                       dbeta);
+                       dbeta, dxsum);
     IC_CHECK_LAUNCH();
     return IC_OK;
   }
   if (split && C == 192)
-    return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
+    return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   switch (C) {
-    case 64: return gdn_bwd_fused_launch<64>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
-    case 128: return gdn_bwd_fused_launch<128>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
-    case 192: return gdn_bwd_fused_launch<192>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, P, slab, s);
+    case 64: return gdn_bwd_fused_launch<64>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
+    case 128: return gdn_bwd_fused_launch<128>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
+    case 192: return gdn_bwd_fused_launch<192>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
     default: return IC_ERR_ARG;
   }
 }

@@ -153,7 +153,8 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
                   long long P, hipStream_t s, int split = 0);  // split: C = 192 in split arithmetic
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
-                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0);
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0,
+                  float* dxsum = nullptr);  // dxsum: column sums of dx over all pixels (C), when non-null
 
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,

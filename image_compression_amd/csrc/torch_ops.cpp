@@ -212,6 +212,27 @@ std::tuple<Tensor, Tensor, Tensor> gdn_bwd(const Tensor& x, const Tensor& norm, 
   return {dx, dg, dbeta};
 }
 
+// gdn_bwd plus the column sums of dx over all pixels (the producing conv's bias gradient)
+std::tuple<Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum(const Tensor& x, const Tensor& norm, const Tensor& dy,
+                                                       const Tensor& gamma, bool inverse, int64_t math) {
+  check_operand(x, "x");
+  check_operand(dy, "dy");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "gdn_bwd_sum: dy must have x's shape and strides");
+  Tensor dx = at::empty_like(x);
+  Tensor dg = at::empty_like(gamma, at::MemoryFormat::Contiguous);
+  Tensor dbeta = at::empty({x.size(1)}, gamma.options());
+  Tensor dxsum = at::empty({x.size(1)}, gamma.options());
+  const ic_act ax = act_of(x), adx = act_of(dx);
+  const size_t nb = ic_gdn_bwd_ws(&ax);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_gdn_bwd_sum_ex(&ax, norm.data_ptr<float>(), dy.data_ptr<float>(), gamma.data_ptr<float>(),
+                             inverse ? 1 : 0, &adx, dg.data_ptr<float>(), dbeta.data_ptr<float>(),
+                             dxsum.data_ptr<float>(), (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "gdn_bwd_sum");
+  return {dx, dg, dbeta, dxsum};
+}
+
 // ---------------------------------------------------------------- shape (Meta) kernels
 Tensor conv2d_fwd_meta(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&, int64_t stride, int64_t pad,
                        int64_t, int64_t) {
@@ -248,6 +269,12 @@ std::tuple<Tensor, Tensor, Tensor> gdn_bwd_meta(const Tensor& x, const Tensor&, 
   return {at::empty_like(x), at::empty_like(gamma, at::MemoryFormat::Contiguous), at::empty({x.size(1)}, gamma.options())};
 }
 
+std::tuple<Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_meta(const Tensor& x, const Tensor&, const Tensor&,
+                                                            const Tensor& gamma, bool, int64_t) {
+  return {at::empty_like(x), at::empty_like(gamma, at::MemoryFormat::Contiguous), at::empty({x.size(1)}, gamma.options()),
+          at::empty({x.size(1)}, gamma.options())};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(imgcomp, m) {
@@ -262,6 +289,8 @@ TORCH_LIBRARY(imgcomp, m) {
         "(Tensor, Tensor)");
   m.def("gdn_fwd(Tensor x, Tensor gamma, Tensor beta, bool inverse, int math) -> (Tensor, Tensor)");
   m.def("gdn_bwd(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> (Tensor, Tensor, Tensor)");
+  m.def("gdn_bwd_sum(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> "
+        "(Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm's HIP device key
@@ -273,6 +302,7 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("conv_transpose2d_wgrad", conv_transpose2d_wgrad);
   m.impl("gdn_fwd", gdn_fwd);
   m.impl("gdn_bwd", gdn_bwd);
+  m.impl("gdn_bwd_sum", gdn_bwd_sum);
 }
 
 TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
@@ -284,4 +314,5 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("conv_transpose2d_wgrad", conv_transpose2d_wgrad_meta);
   m.impl("gdn_fwd", gdn_fwd_meta);
   m.impl("gdn_bwd", gdn_bwd_meta);
+  m.impl("gdn_bwd_sum", gdn_bwd_sum_meta);
 }

@@ -10,6 +10,8 @@ Layout convention: activations with >= 32 channels live in NHWC
 3-channel image tensors stay NCHW and take the generic gather path.
 """
 import ctypes
+import os
+import weakref
 
 import torch
 from torch.autograd import Function
@@ -98,6 +100,30 @@ def _log_plan(op, a, b, k=1, stride=1, pad=0, math=0):
 
 
 # ============================================================== convolutions
+# Column sums of a gradient computed by the op that produced it (GDN backward: sum over pixels
+# of dx), handed to the conv whose output received that gradient, which then skips its own
+# bias-gradient pass over the same tensor.  Keyed by the gradient tensor itself (weakref +
+# version counter): a gradient changed in between (or any other tensor) falls back to the pass.
+_COLSUMS = {}
+_HANDOFF = os.environ.get("IMGCOMP_COLSUM_HANDOFF", "1") != "0"  # 0: every conv takes its own pass (A/B)
+
+
+def _put_colsum(t, s):
+    if not _HANDOFF:
+        return
+    for k in [k for k, (r, _, _) in _COLSUMS.items() if r() is None]:
+        del _COLSUMS[k]
+    _COLSUMS[t.data_ptr()] = (weakref.ref(t), t._version, s)
+
+
+def _take_colsum(t):
+    e = _COLSUMS.pop(t.data_ptr(), None)
+    if e is None:
+        return None
+    r, ver, s = e
+    return s if (r() is t and t._version == ver) else None
+
+
 class Conv2dFn(Function):
     """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56), each
     launch one torch.ops.imgcomp op (csrc/torch_ops.cpp -> C ABI)."""
@@ -120,6 +146,7 @@ class Conv2dFn(Function):
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
         stride, padding, act, has_b, math = ctx.conf
+        pre = _take_colsum(gy) if (has_b and not act) else None  # bias gradient formed by gy's producer
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
@@ -129,9 +156,9 @@ class Conv2dFn(Function):
             dx = ops.conv2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b, math)
+            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
             _log_plan("conv2d_wgrad", x, gy, k, stride, padding, math)
-            db = db if has_b else None
+            db = (db if pre is None else pre) if has_b else None
         return dx, dw, db, None, None, None, None
 
 
@@ -156,6 +183,7 @@ class ConvTranspose2dFn(Function):
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
         stride, padding, act, has_b, math = ctx.conf
+        pre = _take_colsum(gy) if (has_b and not act) else None  # bias gradient formed by gy's producer
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
@@ -165,9 +193,9 @@ class ConvTranspose2dFn(Function):
             dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b, math)
+            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
             _log_plan("conv_transpose2d_wgrad", x, gy, k, stride, padding, math)
-            db = db if has_b else None
+            db = (db if pre is None else pre) if has_b else None
         return dx, dw, db, None, None, None, None, None
 
 
@@ -209,7 +237,10 @@ class GDNFn(Function):
     def backward(ctx, gy):
         x, norm, g = ctx.saved_tensors
         gy = _match(gy, x)
-        dx, dg, dbeta = _lib.ops().gdn_bwd(x, norm, gy, g, ctx.inverse, ctx.math)
+        # dx's column sums come with it (the fused backward forms them from its dx tiles): the
+        # bias gradient of the conv that produced x, taken by that conv's backward (_take_colsum)
+        dx, dg, dbeta, dxsum = _lib.ops().gdn_bwd_sum(x, norm, gy, g, ctx.inverse, ctx.math)
+        _put_colsum(dx, dxsum)
         _log_plan("gdn_bwd", x, None, math=ctx.math)
         return dx, dg, dbeta, None, None, None
 

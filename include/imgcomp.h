@@ -141,6 +141,13 @@ int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int in
 #define IC_MATH_GDN_BWD_FULL_SPLIT 8
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
+/* ic_gdn_bwd_ex plus dxsum[c] = sum over all pixels of dx[.,c,.,.] (C floats): the bias gradient of
+ * the convolution that produced the GDN input (reference analysis.py / synthesis.py: conv -> GDN),
+ * formed by the fused backward from its dx tiles instead of a separate pass over dx.  Same workspace
+ * as ic_gdn_bwd_ws. */
+int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, int math, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* ---- launch-plan query: which kernel instance, tile and K / pixel split a conv or GDN op would launch
  *      for these shapes (no launch, no device access; the same decision code as the launching entry

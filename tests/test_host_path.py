@@ -102,3 +102,18 @@ def test_device_input_conversion_matches_reference_transform():
     assert torch.allclose(y, ref, rtol=1e-6, atol=1e-7)
     y0 = to_device_input(u8, "cuda").cpu()
     assert torch.equal(y0, u8.float().permute(0, 3, 1, 2) / 255.0)
+
+
+def test_colsum_handoff_is_keyed_by_the_gradient_itself():
+    """functional._put_colsum / _take_colsum: a stashed column sum is handed only to the very
+    gradient tensor it was formed from, unchanged since (version counter), and only once."""
+    import torch
+    from image_compression_amd import functional as IF
+    t, s = torch.zeros(4, 3), torch.ones(3)
+    IF._put_colsum(t, s)
+    assert IF._take_colsum(torch.zeros(4, 3)) is None      # another tensor
+    IF._put_colsum(t, s)
+    assert IF._take_colsum(t) is s and IF._take_colsum(t) is None   # once
+    IF._put_colsum(t, s)
+    t.add_(1.0)                                               # changed after the sums were formed
+    assert IF._take_colsum(t) is None

@@ -277,3 +277,44 @@ def test_ms_ssim(log_scale, hw):
     l.sum().backward()
     assert_close(l.detach().cpu().numpy(), lr.detach().numpy(), 1e-4, "ssim")
     assert_close(bd.grad.cpu().numpy(), br2.grad.numpy(), 1e-4, "dssim")
+
+
+@pytest.mark.parametrize("C,H,W,math", [(192, 16, 16, 2), (192, 9, 7, 0), (128, 8, 8, 0), (64, 5, 6, 0), (48, 4, 4, 0)])
+def test_gdn_bwd_dx_column_sums(C, H, W, math):
+    """gdn_bwd_sum: dx as gdn_bwd, plus dxsum[c] = sum over pixels of dx (the producing conv's
+    bias gradient, formed by the fused backward from its dx tiles; C = 48 takes the GEMM path,
+    which sums dx in a separate pass)."""
+    from image_compression_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(3, C, H, W, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    gamma = (0.1 * torch.eye(C) + 0.01 * torch.rand(C, C, generator=g)).reshape(C, C, 1, 1).to(DEV)
+    beta = (1.0 + torch.rand(C, generator=g)).to(DEV)
+    y, norm = _lib.ops().gdn_fwd(x, gamma, beta, False, 0)
+    dy = torch.randn(x.shape, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    dx, dg, db = _lib.ops().gdn_bwd(x, norm, dy, gamma, False, math)
+    dx2, dg2, db2, dxs = _lib.ops().gdn_bwd_sum(x, norm, dy, gamma, False, math)
+    assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+    ref = dx.double().sum(dim=(0, 2, 3))
+    assert ((dxs.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_conv_bias_from_gdn_column_sums():
+    """conv -> GDN: the conv's bias gradient taken from the GDN backward's dx column sums equals
+    the conv's own pass over its output gradient (and conv -> ReLU -> GDN keeps its own pass)."""
+    from image_compression_amd import functional as IF
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(2, 192, 16, 16, generator=g).to(DEV)
+    w = (0.05 * torch.randn(192, 192, 5, 5, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(192, generator=g)).to(DEV)
+    gamma = (0.1 * torch.eye(192) + 0.001).reshape(192, 192, 1, 1).to(DEV)
+    beta = torch.ones(192, device=DEV)
+    gout = torch.randn(2, 192, 8, 8, generator=g).to(DEV)
+    grads = []
+    for fused in (True, False):
+        bb = b.clone().requires_grad_(True)
+        h = IF.conv2d(x, w, bb, 2, 2)
+        if not fused:
+            h = h * 1.0  # another op between: the conv's own bias pass
+        IF.gdn(h, gamma, beta).backward(gout)
+        grads.append(bb.grad.double())
+    assert ((grads[0] - grads[1]).abs().max() / grads[1].abs().max()).item() < 1e-5
