@@ -213,34 +213,40 @@ __global__ void __launch_bounds__(256, 2)
 // v_mfma_f32_16x16x32_bf16 products, fp32 accumulation), C = 192.  12 waves
 // (768 threads), one block per CU: wave w owns output channels [16w, 16w+16)
 // and keeps its slice of Gamma, split into three bf16 terms, as B fragments in
-// 72 VGPRs for the whole launch.  Per 32-pixel tile: LDS-DMA of x (two
-// buffers, as the fp32 kernel), one cooperative pass squares x and writes x^2
-// as three bf16 planes (384-B rows, 16-B chunks XOR (row >> 1) & 7: conflict-
-// free 16x16x32 fragment reads), the MFMAs, the epilogue (y over x in place,
-// norm into a staging image), one coalesced copy-out.
+// 72 VGPRs for the whole launch.  Per 32-pixel tile one cooperative pass
+// squares x and writes x^2 as three bf16 planes (384-B rows, 16-B chunks XOR
+// (row >> 1) & 7: conflict-free 16x16x32 fragment reads), then the MFMAs and
+// the epilogue.  Three x buffers and two sets of x^2 planes (144 KB), so one
+// barrier per tile separates
+//   loads of tile i+3 | split pass of tile i+1 | MFMAs + epilogue of tile i
+// and the waves' split work (VALU, LDS) overlaps the other waves' MFMAs.  x is
+// staged through registers (loaded three tiles ahead of its MFMAs, written to
+// LDS one tile after its loads issued), not by LDS-DMA: the compiler cannot tell an LDS-DMA target
+// from the buffers being read and would wait for the DMA before every LDS read.
+// y and norm leave straight from the MFMA result registers (each 16-lane group
+// writes 64 contiguous bytes of a pixel row; the 12 waves fill the row): no norm
+// staging image and no copy-out pass.
 template <int C>
 __global__ void __launch_bounds__(768, 1)
-    gdn_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
-                      const float* __restrict__ beta, int inverse, float* __restrict__ y,
-                      float* __restrict__ norm, uint32_t P) {
+    gdn_fwd_x3s_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                       const float* __restrict__ beta, int inverse, float* __restrict__ y,
+                       float* __restrict__ norm, uint32_t P) {
   static_assert(C == 192, "12 waves x 16 channels");
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   constexpr int BM = 32, NT = 768;
   constexpr int TILE = BM * C;
-  constexpr int KU = C / 32;                       // 32-wide K chunks
-  constexpr int NSTORE = 2 * (BM * C / 4 / NT);    // vector-memory ops of one copy-out
-  constexpr int QS = BM * C / 4 / NT;              // float4 per thread in the split pass
-  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];  // 2 x-buffers + norm staging
-  __shared__ __attribute__((aligned(16))) __bf16 sq[3 * TILE];   // x^2, three bf16 planes
-  float* const nst = lds + 2 * TILE;
+  constexpr int KU = C / 32;
+  constexpr int QS = BM * C / 4 / NT;  // float4 per thread in staging and in the split pass
+  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];   // three x buffers
+  __shared__ __attribute__((aligned(16))) __bf16 sq[6 * TILE];  // two sets of three x^2 planes
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
-  const int n = 16 * w + li;  // this lane's output channel (B column / C/D column)
+  const int n = 16 * w + li;
   const uint32_t ntiles = (P + BM - 1) / BM;
+  const uint32_t G = gridDim.x;
 
-  // Gamma^T fragments: lane (n = li, g) holds k = 32u + 8g .. +7 of row n of Gamma
   b8 bg[3][KU];
 #pragma unroll
   for (int u = 0; u < KU; ++u) {
@@ -253,50 +259,77 @@ __global__ void __launch_bounds__(768, 1)
       bg[0][u][e] = hh; bg[1][u][e] = mm; bg[2][u][e] = ll;
     }
   }
-  const float bet = beta[n];
-  const int fsw = (li >> 1) & 7;  // fragment rows 16mt + li share bits 1..3 of li
+  float bet = beta[n];
+  // consume the prologue's loads here: a load still pending at the loop entry makes the compiler
+  // wait for every store of the previous tile inside the loop
+  asm volatile("" : "+v"(bet));
+  const int fsw = (li >> 1) & 7;
 
-  uint32_t tile = blockIdx.x;
-  if (tile < ntiles) stage_tile<C, BM, NT>(x, tile * BM, P, lds, tid, lane);
-  int buf = 0;
-  bool first = true;
-  for (; tile < ntiles; tile += gridDim.x) {
-    if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
-    __builtin_amdgcn_s_barrier();  // B1: tile `buf` landed
-    first = false;
-    const uint32_t nxt = tile + gridDim.x;
-    float* xs = lds + buf * TILE;
-    if (nxt < ntiles) stage_tile<C, BM, NT>(x, nxt * BM, P, lds + (buf ^ 1) * TILE, tid, lane);
-    // x^2 split pass: float4 `pos` of the swizzled fp32 image -> 3 bf16 quads
+  // staging: float4 `pos` of a swizzled image holds logical chunk (pos % (C/4)) ^ (row & 15)
+  int srow[QS], scol[QS];
+#pragma unroll
+  for (int q = 0; q < QS; ++q) {
+    const int pos = tid + NT * q;
+    srow[q] = pos / (C / 4);
+    scol[q] = ((pos - srow[q] * (C / 4)) ^ (srow[q] & 15)) * 4;
+  }
+  // rows past P load row P-1 (a row's x^2 feeds only that row's outputs, which are not stored)
+  auto load = [&](uint32_t t, floatx4v* r) {
+#pragma unroll
+    for (int q = 0; q < QS; ++q) {
+      const uint32_t m = min(t * BM + srow[q], P - 1);
+      r[q] = *(const floatx4v*)(x + (size_t)m * C + scol[q]);
+    }
+  };
+  auto put = [&](float* img, const floatx4v* r) {
+#pragma unroll
+    for (int q = 0; q < QS; ++q) *(floatx4v*)(img + (tid + NT * q) * 4) = r[q];
+  };
+  // x^2 split pass: float4 `pos` of a swizzled fp32 image -> 3 bf16 quads
+  auto split_pass = [&](const float* xs, __bf16* sb) {
 #pragma unroll
     for (int q = 0; q < QS; ++q) {
       const int pos = tid + NT * q;
-      const int m = pos / (C / 4), lc = (pos - m * (C / 4)) ^ (m & 15);
+      const int m = srow[q], lc = scol[q] >> 2;
       const floatx4v v = *(const floatx4v*)(xs + pos * 4);
       b4 vh, vm, vl;
-      if (GDN_SPLIT_PK) {
-        split3_bf16x4(v * v, vh, vm, vl);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          __bf16 hh, mm, ll;
-          split3_bf16(v[e] * v[e], hh, mm, ll);
-          vh[e] = hh; vm[e] = mm; vl[e] = ll;
-        }
-      }
+      split3_bf16x4(v * v, vh, vm, vl);
       const int off = m * C + 8 * ((lc >> 1) ^ ((m >> 1) & 7)) + 4 * (lc & 1);
-      *(b4*)(sq + off) = vh;
-      *(b4*)(sq + TILE + off) = vm;
-      *(b4*)(sq + 2 * TILE + off) = vl;
+      *(b4*)(sb + off) = vh;
+      *(b4*)(sb + TILE + off) = vm;
+      *(b4*)(sb + 2 * TILE + off) = vl;
     }
+  };
+
+  uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  floatx4v ra[QS], rb[QS];  // staging registers, two tiles in flight (loaded 2 tiles ahead of use)
+  load(tile, ra);
+  put(lds, ra);
+  load(tile + G < ntiles ? tile + G : tile, ra);
+  put(lds + TILE, ra);
+  load(tile + 2 * G < ntiles ? tile + 2 * G : tile, rb);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  split_pass(lds, sq);
+  int bx = 0, sb = 0;  // x buffer of `tile` (next: bx+1, staging: bx+2, mod 3); its plane set
+  // one tile: load tile+3G into `ld` (a tile past the end reloads this one: no branch, so the
+  // compiler counts the loads and stores and never waits for the stores), write `pt` (tile+2G,
+  // loaded one tile earlier) into the free buffer at the end
+  auto step = [&](floatx4v* ld, const floatx4v* pt) {
+    // plane set sb and x buffer bx+1 complete; every wave's reads of the buffers written below done
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // B2: x^2 planes complete
+    __builtin_amdgcn_s_barrier();
+    const int b1 = bx == 2 ? 0 : bx + 1, b2 = b1 == 2 ? 0 : b1 + 1;
+    load(tile + 3 * G < ntiles ? tile + 3 * G : tile, ld);
+    if (tile + G < ntiles) split_pass(lds + b1 * TILE, sq + (sb ^ 1) * 3 * TILE);
+    const float* xs = lds + bx * TILE;
+    const __bf16* sp = sq + sb * 3 * TILE;
     floatx4v acc[BM / 16];
 #pragma unroll
     for (int mt = 0; mt < BM / 16; ++mt) {
       acc[mt] = floatx4v{0.f, 0.f, 0.f, 0.f};
-      const __bf16* ar = sq + (16 * mt + li) * C;
+      const __bf16* ar = sp + (16 * mt + li) * C;
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         const int ch = 8 * ((4 * u + lg) ^ fsw);
@@ -309,24 +342,29 @@ __global__ void __launch_bounds__(768, 1)
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[0][u], acc[mt], 0, 0, 0);
       }
     }
-    // epilogue (C/D map: col n = li, row m = 16mt + 4g + r); y over x in place
+    // epilogue (C/D map: col n = li, row m = 16mt + 4g + r) straight to y and norm; rows past P
+    // hold row P-1's x, so their results equal row P-1's and are stored there (the same values)
+    const uint32_t m0 = tile * BM;
 #pragma unroll
     for (int mt = 0; mt < BM / 16; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int off = swz<C>(16 * mt + 4 * lg + r, n);
-        const float nv = acc[mt][r] + bet;
-        const float xv = xs[off];
-        xs[off] = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
-        nst[off] = nv;
+      for (int q = 0; q < 4; ++q) {
+        const int m = 16 * mt + 4 * lg + q;
+        const float nv = acc[mt][q] + bet;
+        const float xv = xs[swz<C>(m, n)];
+        const float yv = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
+        const size_t o = (size_t)min(m0 + m, P - 1) * C + n;
+        y[o] = yv;
+        norm[o] = nv;
       }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // B3
-    store_tile<C, BM, NT>(y, tile * BM, P, xs, tid);
-    store_tile<C, BM, NT>(norm, tile * BM, P, nst, tid);
-    buf ^= 1;
+    put(lds + b2 * TILE, pt);
+    bx = b1;
+    sb ^= 1;
+    tile += G;
+    return tile < ntiles;
+  };
+  while (step(ra, rb) && step(rb, ra)) {
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ============================================================== backward
@@ -997,7 +1035,7 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
     const long long ntiles = (P + 31) / 32;
     const long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
     if (grid < 1) return IC_OK;
-    hipLaunchKernelGGL((gdn_fwd_x3_kernel<192>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse, y,
+    hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse, y,
                        norm, (uint32_t)P);
     IC_CHECK_LAUNCH();
     return IC_OK;
