@@ -44,8 +44,31 @@ __device__ __attribute__((aligned(16))) float gdn_zero_page[4];
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
+// 16 B per lane global -> LDS (M0 = the wave's LDS base; M0 restored after).  Issued from
+// inline asm rather than __builtin_amdgcn_global_load_lds: for the builtin, the compiler cannot
+// tell the DMA's LDS target from the buffers being read and waits vmcnt(0) before the next LDS
+// read, which puts the whole DMA latency of the next tile on the current tile's path.  The
+// kernels wait for these loads explicitly (s_waitcnt vmcnt before the barrier that publishes a
+// tile).
+#ifndef GDN_DMA_ASM
+#define GDN_DMA_ASM 1
+#endif
 __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+  if (!GDN_DMA_ASM) {
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+    return;
+  }
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)lds_wave_base);
+  uint32_t save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "v"(src), "s"(l)
+      : "memory");
 }
 
 // element (m, n) of a swizzled [rows][C] tile image
