@@ -50,6 +50,9 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 // read, which puts the whole DMA latency of the next tile on the current tile's path.  The
 // kernels wait for these loads explicitly (s_waitcnt vmcnt before the barrier that publishes a
 // tile).
+#ifndef GDN_BWD_DMA_B
+#define GDN_BWD_DMA_B 1  // fused backward: group B issues the next tile's DMA (0: group A, after its first MFMAs)
+#endif
 #ifndef GDN_DMA_ASM
 #define GDN_DMA_ASM 1
 #endif
@@ -516,6 +519,17 @@ __global__ void __launch_bounds__(512, 2)
   const int wbase = (w & 3) * W4;
   const uint32_t ntiles = (P + BM - 1) / BM;
 
+  // group B issues the next tile's DMA (not in the fp32 C = 192 kernel, whose group B holds a
+  // 144-register dgamma and would spill)
+  constexpr bool DMA_B = GDN_BWD_DMA_B && (X3 || C < 192);
+  // x, norm, dy of tile t into buffer b (256 threads; ti = thread index within the group)
+  auto stage = [&](uint32_t t, int b, int ti) {
+    float* base = lds + b * 3 * TILE;
+    stage_tile<C, BM, NTA>(x, t * BM, P, base, ti, lane);
+    stage_tile<C, BM, NTA>(norm, t * BM, P, base + TILE, ti, lane);
+    stage_tile<C, BM, NTA>(dy, t * BM, P, base + 2 * TILE, ti, lane);
+  };
+
   if (w < 4) {
     // ---------------- group A: dxg[m][k] = sum_n q[m][n] gamma[n][k], k = wbase + 16j + li
     // step s = 4u+v: n = 16u + 4lq + v  ->  bfr[j][4u+v] = gamma[n][k]
@@ -527,14 +541,8 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           bfr[j][4 * u + v] = gamma[(size_t)(16 * u + 4 * lq + v) * C + wbase + 16 * j + li];
-    auto stage = [&](uint32_t t, int b) {
-      float* base = lds + b * 3 * TILE;
-      stage_tile<C, BM, NTA>(x, t * BM, P, base, tid, lane);
-      stage_tile<C, BM, NTA>(norm, t * BM, P, base + TILE, tid, lane);
-      stage_tile<C, BM, NTA>(dy, t * BM, P, base + 2 * TILE, tid, lane);
-    };
     uint32_t tile = blockIdx.x;
-    if (tile < ntiles) stage(tile, 0);
+    if (tile < ntiles) stage(tile, 0, tid);
     int buf = 0, it = 0;
     bool first = true;
     for (; tile < ntiles; tile += gridDim.x, ++it) {
@@ -561,11 +569,11 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
           for (int j = 0; j < NTW; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[v], bfr[j][4 * u + v], acc[j], 0, 0, 0);
-        if (u == 0) {
+        if (!DMA_B && u == 0) {
           // the next tile's DMA issues behind the first MFMAs instead of on the
           // barrier-to-barrier critical path (buffer buf^1 is free since B1)
           __builtin_amdgcn_sched_barrier(0);
-          if (nxt < ntiles) stage(nxt, buf ^ 1);
+          if (nxt < ntiles) stage(nxt, buf ^ 1, tid);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -620,6 +628,9 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
+      // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
+      // is free since B1, and this group's wait before the next B1 covers it
+      if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
       gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
@@ -690,6 +701,9 @@ __global__ void __launch_bounds__(512, 2)
       GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
+      // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
+      // is free since B1, and this group's wait before the next B1 covers it
+      if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
       gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
