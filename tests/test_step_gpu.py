@@ -103,7 +103,9 @@ def test_concurrent_step_repeatable_at_c2():
     stream crossings (bmshl2018._StreamEdge): without the gradients recorded on their
     consumer stream the caching allocator handed a gradient's memory to the other stream's
     next allocation while it was still read, and about one step in five came out with a
-    changed CDF-estimator weight gradient element (tools/determinism_probe.py)."""
+    changed CDF-estimator weight gradient element (tools/determinism_probe.py).  Each run drops
+    its graph before the next one (see below): a serial run's AccumulateGrad nodes kept alive into
+    a concurrent run make torch accumulate side-stream gradients on the main stream."""
     from image_compression_amd import get_cfg_defaults, injected_noise, modelling
     cfg = get_cfg_defaults()
     cfg.MODEL.LOSS.REDUCTION = "mean"
@@ -116,14 +118,22 @@ def test_concurrent_step_repeatable_at_c2():
     uz = torch.rand(32, 192, 4, 4, generator=g).to(DEV)
     uy = torch.rand(32, 192, 16, 16, generator=g).to(DEV)
     runs = []
-    for conc in [False] + [True] * 8:
-        m.concurrent_hyperprior = conc
-        m.zero_grad(set_to_none=True)
-        with injected_noise([uz, uy]):
-            _, losses = m(x)
-            losses["total_loss"].backward()
-        torch.cuda.synchronize()
-        runs.append({k: p.grad.clone() for k, p in m.named_parameters()})
+    import warnings
+    with warnings.catch_warnings():
+        # a stream mismatch would mean an AccumulateGrad node outlived its run (see below)
+        warnings.filterwarnings("error", message="The AccumulateGrad node's stream does not match")
+        for conc in [False] + [True] * 8:
+            m.concurrent_hyperprior = conc
+            m.zero_grad(set_to_none=True)
+            with injected_noise([uz, uy]):
+                xt, losses = m(x)
+                losses["total_loss"].backward()
+            # drop the graph: a live graph keeps the parameters' AccumulateGrad nodes, and a node
+            # made by the serial run (main stream) would then accumulate the side stream's
+            # gradients of the next, concurrent run on the main stream
+            del xt, losses
+            torch.cuda.synchronize()
+            runs.append({k: p.grad.clone() for k, p in m.named_parameters()})
     for i, r in enumerate(runs[1:], 1):
         for k, v in r.items():
             assert torch.equal(v, runs[0][k]), (i, k)
