@@ -279,7 +279,8 @@ def test_ms_ssim(log_scale, hw):
     assert_close(bd.grad.cpu().numpy(), br2.grad.numpy(), 1e-4, "dssim")
 
 
-@pytest.mark.parametrize("C,H,W,math", [(192, 16, 16, 2), (192, 9, 7, 0), (128, 8, 8, 0), (64, 5, 6, 0), (48, 4, 4, 0)])
+@pytest.mark.parametrize("C,H,W,math", [(192, 16, 16, 2), (192, 9, 7, 0), (128, 8, 8, 0), (64, 5, 6, 0), (48, 4, 4, 0),
+                                          (192, 67, 61, 2)])
 def test_gdn_bwd_dx_column_sums(C, H, W, math):
     """gdn_bwd_sum: dx as gdn_bwd, plus dxsum[c] = sum over pixels of dx (the producing conv's
     bias gradient, formed by the fused backward from its dx tiles; C = 48 takes the GEMM path,

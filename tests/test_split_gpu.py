@@ -203,7 +203,7 @@ def test_gdn_split_dgamma(n, h, w, inverse):
 
 # (8, 192, 67, 65): 1,089 32-pixel tiles, 4-5 per block of the pipelined split kernel, last one partial
 @pytest.mark.parametrize("n,c,h,w,inverse", [(2, 192, 16, 16, False), (3, 192, 7, 5, True), (2, 64, 9, 9, False),
-                                             (8, 192, 67, 65, True)])
+                                             (8, 192, 67, 65, True), (6, 192, 90, 77, False)])
 def test_gdn_split_forward(n, c, h, w, inverse):
     """GDN forward with math_fwd 2: norm = beta + Gamma x^2 on the split implicit GEMM."""
     from image_compression_amd.modelling.layers import GDN
