@@ -185,7 +185,7 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
                                        weight gradient in split arithmetic */
 #define IC_KERNEL_EDGE_WGRAD 15     /* edge_wgrad_kernel */
 #define IC_KERNEL_GDN_FUSED 16      /* gdn_fwd_fused_kernel / gdn_bwd_fused_kernel (fp32 dx) */
-#define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3_kernel / gdn_bwd_fused_kernel with split dgamma */
+#define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3s_kernel / gdn_bwd_fused_kernel with split dgamma */
 #define IC_KERNEL_GDN_GEMM 18       /* GDN on the implicit GEMM (+ wgrad kernel for dgamma) */
 typedef struct ic_plan {
   int kernel;        /* IC_KERNEL_* of the main launch */
