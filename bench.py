@@ -121,7 +121,7 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     pm = _mfma_peak_measured()
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
-        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,true,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
+        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
     else:
         peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
@@ -300,10 +300,6 @@ def main():
     # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
-    if dist:
-        # the hyperprior side stream is measured and tested at one rank; under DDP the gradient
-        # hooks keep the single-stream backward that the multi-rank path was built and tested on
-        model.concurrent_hyperprior = False
     if not args.graph:
         model = D.wrap(model, dev)
 

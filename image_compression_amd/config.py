@@ -66,7 +66,7 @@ _DEFAULTS = {
              "MEAN": [0., 0., 0.], "STD": [1., 1., 1.], "TRAIN_DATASET_NAME": "", "VAL_DATASET_NAME": "",
              "DATALOADER_NAME": "infinite_dataloader"},
     "MODEL": {
-        "META_ARCHITECTURE": "Compressor2018", "COMPUTE_DTYPE": "fp32",
+        "META_ARCHITECTURE": "Compressor2018", "COMPUTE_DTYPE": "fp32_split",
         "STRIDES": [2, 2, 2, 2], "CONV_KERNEL": 5, "INTER_CHANNELS": 192, "LATENT_CHANNELS": 192,
         "HYPER_PRIOR": {"STRIDES": [1, 2, 2], "KERNELS": [3, 5, 5]},
         "ENTROPY_MODEL": {"DIMS": [3, 3, 3], "INIT_SCALE": 10, "BIN": 1., "PROB_EPS": 1e-10,

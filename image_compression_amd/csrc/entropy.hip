@@ -578,6 +578,7 @@ extern "C" {
 int ic_factorized_fwd(const float* z, long long n, int C, const ic_fact_params* prm, int mode, const float* u,
                       unsigned long long seed, unsigned long long offset, float* q, float* p, void* stream) {
   if (C <= 0 || n % C != 0 || (mode == 0 && !u)) return IC_ERR_ARG;
+  if ((mode == 2 || mode == 3) && (offset & 3)) return IC_ERR_ARG;  // whole Philox blocks
   hipLaunchKernelGGL(fact_fwd_k, dim3(C), dim3(256), 0, (hipStream_t)stream, z, n, C, *prm, mode, u, seed,
                      offset, q, p);
   IC_CHECK_LAUNCH();
@@ -595,7 +596,7 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
 int ic_quantize(const float* y, long long n, int mode, const float* u, unsigned long long seed,
                 unsigned long long offset, float bin, float* q, void* stream) {
   if ((mode == 0 && !u) || mode < 0 || mode > 3 || !(bin > 0.f)) return IC_ERR_ARG;
-  if (mode == 2 && (offset & 3)) return IC_ERR_ARG;
+  if ((mode == 2 || mode == 3) && (offset & 3)) return IC_ERR_ARG;  // whole Philox blocks (4 draws)
   long long b = (n + 1023) / 1024;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
@@ -610,7 +611,7 @@ int ic_conditional_fwd_bin(const float* y, const float* scale, const float* mean
                            float* p, void* stream) {
   if ((mode == 0 && !u) || mode < 0 || mode > 4) return IC_ERR_ARG;
   if (!(bin > 0.f)) return IC_ERR_ARG;
-  if (mode == 2 && (offset & 3)) return IC_ERR_ARG;  // stream offsets are whole Philox blocks
+  if ((mode == 2 || mode == 3) && (offset & 3)) return IC_ERR_ARG;  // stream offsets are whole Philox blocks
   long long b = (n + 1023) / 1024;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
@@ -647,6 +648,7 @@ int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net*
                           const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
                           void* stream) {
   if (C <= 0 || n % C != 0 || (mode == 0 && !u) || !fact_net_ok(net) || !(bin > 0.f)) return IC_ERR_ARG;
+  if ((mode == 2 || mode == 3) && (offset & 3)) return IC_ERR_ARG;  // whole Philox blocks
   hipLaunchKernelGGL(fact_fwd_net_k, dim3(C), dim3(FNT), fact_net_lds(net, false), (hipStream_t)stream, z, n, C,
                      *net, 0.5f * bin, mode, u, seed, offset, q, p);
   IC_CHECK_LAUNCH();

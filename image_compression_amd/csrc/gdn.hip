@@ -105,7 +105,7 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
       wsb >= fused_ws)
     return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s,
-                         (math & IC_MATH_SPLIT) ? ((math & IC_MATH_GDN_BWD_FULL_SPLIT) ? 2 : 1) : 0, dxsum);
+                         (math & IC_MATH_SPLIT) ? 1 : 0, dxsum);
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};

@@ -780,209 +780,6 @@ __global__ void __launch_bounds__(512, 2)
 }
 
 
-// ============================================================== backward, split (C = 192)
-// The whole backward in split arithmetic (fp32 via three bf16 terms, six
-// products per MAC, fp32 accumulation), one block of 12 waves per CU.
-// Wave w owns dx columns k in [16w, 16w+16) — its slice of Gamma (B[n][k] =
-// Gamma[n][k], 8 consecutive n per lane), split, lives in 72 VGPRs — and
-// three 32x32 tiles of dgamma (48 accumulator VGPRs).  Per 16-pixel tile:
-// LDS-DMA of x, norm, dy (two buffers); phase A (one float4 per thread)
-// forms q = dL/dnorm, the direct term over dy, a dbeta partial in registers,
-// and writes q and x^2 as split bf16 [pixel][channel] images whose 16-B
-// chunks are XOR-swizzled by gdn_bsw(row) — conflict-free for both the
-// row reads of the dx GEMM (16x16x32) and the transposed reads
-// (ds_read_b64_tr_b16) of the dgamma GEMM (32x32x16); then both GEMMs, the
-// dx epilogue over the direct term in place, one coalesced copy-out.
-__device__ __forceinline__ int gdn_bsw(int r) { return (0x62624040u >> (4 * ((r >> 1) & 7))) & 7; }
-
-template <int C>
-__global__ void __launch_bounds__(768, 1)
-    gdn_bwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
-                      const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
-                      float* __restrict__ slab, uint32_t P) {
-  static_assert(C == 192, "12 waves x 16 dx columns, 36 dgamma tiles of 32x32");
-  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-  constexpr int BM = 16, NT = 768;
-  constexpr int TILE = BM * C;           // elements of one image
-  constexpr int KU = C / 32;
-  __shared__ __attribute__((aligned(16))) float lds[6 * TILE];      // 2 buffers x (x, norm, dy)
-  __shared__ __attribute__((aligned(16))) __bf16 sb[6 * TILE];      // q planes, x^2 planes
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lg = lane >> 4;
-  const uint32_t ntiles = (P + BM - 1) / BM;
-  const int kcol = 16 * w + li;  // dx column of this lane
-
-  // Gamma slice for dx: lane (k = kcol, g) holds n = 32u + 8g .. +7 of column k
-  b8 bg[3][KU];
-#pragma unroll
-  for (int u = 0; u < KU; ++u)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      __bf16 hh, mm, ll;
-      split3_bf16(gamma[(size_t)(32 * u + 8 * lg + e) * C + kcol], hh, mm, ll);
-      bg[0][u][e] = hh; bg[1][u][e] = mm; bg[2][u][e] = ll;
-    }
-  // dgamma tiles of this wave: T = 3w + t -> rows 32 (T / 6), cols 32 (T % 6)
-  floatx16 dg[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dg[t][e] = 0.f;
-  floatx4v dbp = {0.f, 0.f, 0.f, 0.f};
-  float dxs = 0.f;  // dx column-sum partial of column tid < C
-  // phase-A element of this thread: row pm, logical channel quad plc
-  const int pm = tid / (C / 4), ppc = tid - pm * (C / 4), plc = ppc ^ (pm & 15);
-  const int a_st = pm * C + 8 * ((plc >> 1) ^ gdn_bsw(pm)) + 4 * (plc & 1);
-  // transposed reads (32x32x16): rows 8h + (li >> 2) (+4), columns c0 + 16 (lane>>4 & 1) + 4 (li & 3)
-  const int h = lane >> 5, r32 = lane & 31;
-  const int tr_row = 8 * h + (li >> 2);
-  const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-  auto tr8 = [&](const __bf16* plane, int c0) {
-    // both rows of the pair (tr_row, tr_row + 4) share bits 1..3 -> one swizzle
-    const int sw = gdn_bsw(tr_row);
-    const int col = c0 + tr_col;  // multiple of 4: stays inside its 16-B chunk
-    const int off = tr_row * C + 8 * ((col >> 3) ^ sw) + (col & 7);
-    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + off));
-    const b4 hi =
-        __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + off + 4 * C));
-    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  const int fsw = gdn_bsw(li);  // dx A-fragment rows li
-
-  uint32_t tile = blockIdx.x;
-  auto stage = [&](uint32_t t, int b) {
-    float* base = lds + b * 3 * TILE;
-    stage_tile<C, BM, NT>(x, t * BM, P, base, tid, lane);
-    stage_tile<C, BM, NT>(norm, t * BM, P, base + TILE, tid, lane);
-    stage_tile<C, BM, NT>(dy, t * BM, P, base + 2 * TILE, tid, lane);
-  };
-  if (tile < ntiles) stage(tile, 0);
-  int buf = 0;
-  bool first = true;
-  for (; tile < ntiles; tile += gridDim.x) {
-    // tile `buf` landed (its DMA is older than the previous copy-out's one store)
-    if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // B1
-    first = false;
-    const uint32_t nxt = tile + gridDim.x;
-    if (nxt < ntiles) stage(nxt, buf ^ 1);
-    float* xs = lds + buf * 3 * TILE;
-    float* gs = xs + 2 * TILE;  // dy -> direct term -> dx
-    // ---- phase A
-    {
-      const int off = tid * 4;
-      const bool valid = tile * BM + (uint32_t)pm < P;  // rows past P are zero-filled
-      const floatx4v xv = *(const floatx4v*)(xs + off);
-      const floatx4v nv = *(const floatx4v*)(xs + TILE + off);
-      const floatx4v gv = *(const floatx4v*)(gs + off);
-      floatx4v qv, dv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float rs = __builtin_amdgcn_rsqf(nv[e]);
-        if (inverse) {
-          qv[e] = 0.5f * gv[e] * xv[e] * rs;
-          dv[e] = gv[e] * (nv[e] * rs);
-        } else {
-          qv[e] = -0.5f * gv[e] * xv[e] * (rs * rs * rs);
-          dv[e] = gv[e] * rs;
-        }
-      }
-      if (!valid) {
-        qv = floatx4v{0.f, 0.f, 0.f, 0.f};
-        dv = qv;
-      }
-      *(floatx4v*)(gs + off) = dv;
-      dbp += qv;
-      b4 qh, qm, ql, xh, xm, xl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 a0, a1, a2;
-        split3_bf16(qv[e], a0, a1, a2);
-        qh[e] = a0; qm[e] = a1; ql[e] = a2;
-        split3_bf16(xv[e] * xv[e], a0, a1, a2);
-        xh[e] = a0; xm[e] = a1; xl[e] = a2;
-      }
-      *(b4*)(sb + a_st) = qh;
-      *(b4*)(sb + TILE + a_st) = qm;
-      *(b4*)(sb + 2 * TILE + a_st) = ql;
-      *(b4*)(sb + 3 * TILE + a_st) = xh;
-      *(b4*)(sb + 4 * TILE + a_st) = xm;
-      *(b4*)(sb + 5 * TILE + a_st) = xl;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // B2
-    // ---- dgamma[n][k] += sum_p q[p][n] x[p][k]^2 on this wave's three 32x32 tiles
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int T = 3 * w + t, ti = T / 6, tj = T - (T / 6) * 6;
-      b8 a[3], bq[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        a[q] = tr8(sb + q * TILE, 32 * ti);
-        bq[q] = tr8(sb + (3 + q) * TILE, 32 * tj);
-      }
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bq[0], dg[t], 0, 0, 0);
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[1], dg[t], 0, 0, 0);
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[2], dg[t], 0, 0, 0);
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bq[0], dg[t], 0, 0, 0);
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[1], dg[t], 0, 0, 0);
-      dg[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bq[0], dg[t], 0, 0, 0);
-    }
-    // ---- dxg[p][k] = sum_n q[p][n] Gamma[n][k]: rows = the 16 pixels, column kcol
-    floatx4v ax = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int ch = 8 * ((4 * u + lg) ^ fsw);
-      const b8 q0 = *(const b8*)(sb + li * C + ch), q1 = *(const b8*)(sb + TILE + li * C + ch),
-               q2 = *(const b8*)(sb + 2 * TILE + li * C + ch);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q2, bg[0][u], ax, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q1, bg[1][u], ax, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q0, bg[2][u], ax, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q1, bg[0][u], ax, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q0, bg[1][u], ax, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q0, bg[0][u], ax, 0, 0, 0);
-    }
-    // dx = direct + 2 x dxg (C/D map: col k = kcol, rows 4g + r), over the direct term
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int off = swz<C>(4 * lg + r, kcol);
-      gs[off] = gs[off] + 2.f * xs[off] * ax[r];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // B3
-    store_tile<C, BM, NT>(dx, tile * BM, P, gs, tid);
-    if (tid < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
-      const int rows = (P - tile * BM) < (uint32_t)BM ? (int)(P - tile * BM) : BM;
-      for (int m = 0; m < rows; ++m) dxs += gs[swz<C>(m, tid)];
-    }
-    buf ^= 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  // partials: slab[block][n][k], dbeta [C] (its 16 row partials combine in LDS in a fixed order), dx column sums
-  float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
-  if (tid < C) out[C * C + C + tid] = dxs;
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int T = 3 * w + t, ti = T / 6, tj = T - (T / 6) * 6;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int nrow = 32 * ti + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      out[(size_t)nrow * C + 32 * tj + r32] = dg[t][reg];
-    }
-  }
-  __syncthreads();
-  *(floatx4v*)(lds + pm * C + 4 * plc) = dbp;
-  __syncthreads();
-  if (tid < C) {
-    float v = 0.f;
-    for (int m = 0; m < BM; ++m) v += lds[m * C + tid];
-    out[C * C + tid] = v;
-  }
-}
-
 // fixed-order sum of the per-block partials
 // 64 elements x 4 groups of partials per block; each group sums a quarter of
 // the partials with eight loads in flight, the quarters combine in LDS in a
@@ -1090,19 +887,6 @@ size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * GDN_S
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {
   float* slab = (float*)ws;
-  if (split == 2 && C == 192) {
-    // whole backward in split arithmetic, one 12-wave block per CU
-    const int grid = bwd_grid(P);
-    if (grid < 1) return IC_OK;
-    hipLaunchKernelGGL((gdn_bwd_x3_kernel<192>), dim3(grid), dim3(768), 0, s, x, norm, dy, gamma, inverse, dx, slab,
-                       (uint32_t)P);
-    IC_CHECK_LAUNCH();
-    const int stride = GDN_SLAB(C);
-    hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
-                       dbeta, dxsum);
-    IC_CHECK_LAUNCH();
-    return IC_OK;
-  }
   if (split && C == 192)
     return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   switch (C) {

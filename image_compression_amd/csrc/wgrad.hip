@@ -1018,7 +1018,8 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   if (WG_X3_DUAL && d.rowfast && d.Wg % 32 == 0 && d.pps % 32 == 0) {
     if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false>), grid, dim3(512), 0, s, d);
     else hipLaunchKernelGGL((wg_x3d_kernel<false, false>), grid, dim3(512), 0, s, d);
-  } else if (WG_X3_DUAL16 && d.rowfast && d.Wg % 16 == 0 && d.pps % 32 == 0) {
+  } else if (WG_X3_DUAL16 && d.rowfast && d.Wg % 16 == 0 && d.pps % 32 == 0 && d.P % 32 == 0) {
+    // whole 32-pixel steps only: with P % 32 == 16 the last split would end on half a step
     if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, true>), grid, dim3(512), 0, s, d);
     else hipLaunchKernelGGL((wg_x3d_kernel<false, true>), grid, dim3(512), 0, s, d);
   } else if (d.rowfast) {

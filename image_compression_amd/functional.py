@@ -9,8 +9,7 @@ Layout convention: activations with >= 32 channels live in NHWC
 (torch.channels_last) so every GEMM operand row is channel-contiguous; the
 3-channel image tensors stay NCHW and take the generic gather path.
 """
-import ctypes
-import os
+import threading
 import weakref
 
 import torch
@@ -20,10 +19,6 @@ from . import _lib
 from . import noise as _noise
 
 CL = torch.channels_last
-
-
-def _L():
-    return _lib.load()
 
 
 def _cl(t):
@@ -68,14 +63,6 @@ def _match(g, ref):
     return out
 
 
-def _ws(nbytes, device):
-    return _lib.workspace(nbytes, device)
-
-
-def _n(t):
-    return ctypes.c_longlong(t.numel())
-
-
 # launch-plan log (tests): while a list is installed by `record_plans`, every conv / GDN op
 # appends the plan (ic_conv_plan) of each launch it makes, so a test can show which kernel
 # instances a whole training step ran
@@ -102,22 +89,29 @@ def _log_plan(op, a, b, k=1, stride=1, pad=0, math=0):
 # ============================================================== convolutions
 # Column sums of a gradient computed by the op that produced it (GDN backward: sum over pixels
 # of dx), handed to the conv whose output received that gradient, which then skips its own
-# bias-gradient pass over the same tensor.  Keyed by the gradient tensor itself (weakref +
-# version counter): a gradient changed in between (or any other tensor) falls back to the pass.
+# bias-gradient pass over the same tensor.  Keyed by the gradient tensor itself (device +
+# storage pointer, checked against a weakref and the version counter): a gradient changed in
+# between (or any other tensor) falls back to the pass.  Backward passes of several devices may
+# run concurrently (one autograd thread per device; nn.DataParallel replicas), so the table is
+# locked.
 _COLSUMS = {}
-_HANDOFF = os.environ.get("IMGCOMP_COLSUM_HANDOFF", "1") != "0"  # 0: every conv takes its own pass (A/B)
+_COLSUMS_LOCK = threading.Lock()
+
+
+def _colsum_key(t):
+    return (t.device.index, t.data_ptr())
 
 
 def _put_colsum(t, s):
-    if not _HANDOFF:
-        return
-    for k in [k for k, (r, _, _) in _COLSUMS.items() if r() is None]:
-        del _COLSUMS[k]
-    _COLSUMS[t.data_ptr()] = (weakref.ref(t), t._version, s)
+    with _COLSUMS_LOCK:
+        for k in [k for k, (r, _, _) in _COLSUMS.items() if r() is None]:
+            del _COLSUMS[k]
+        _COLSUMS[_colsum_key(t)] = (weakref.ref(t), t._version, s)
 
 
 def _take_colsum(t):
-    e = _COLSUMS.pop(t.data_ptr(), None)
+    with _COLSUMS_LOCK:
+        e = _COLSUMS.pop(_colsum_key(t), None)
     if e is None:
         return None
     r, ver, s = e
@@ -258,9 +252,7 @@ class NonNegFn(Function):
     def forward(ctx, p, bound, pedestal):
         _lib.require_device(p)
         p = p.contiguous()
-        out = torch.empty_like(p)
-        _lib.check(_L().ic_nonneg_fwd(_lib.ptr(p), _n(p), float(bound), float(pedestal), _lib.ptr(out),
-                                      _lib.stream_of(p)), "nonneg_fwd")
+        out = _lib.ops().nonneg_fwd(p, float(bound), float(pedestal))
         ctx.bound = float(bound)
         ctx.save_for_backward(p)
         return out
@@ -268,23 +260,19 @@ class NonNegFn(Function):
     @staticmethod
     def backward(ctx, g):
         (p,) = ctx.saved_tensors
-        g = _match(g, p)
-        gi = torch.empty_like(p)
-        _lib.check(_L().ic_nonneg_bwd(_lib.ptr(p), _lib.ptr(g), _n(p), ctx.bound, _lib.ptr(gi),
-                                      _lib.stream_of(p)), "nonneg_bwd")
-        return gi, None, None
+        return _lib.ops().nonneg_bwd(p, _match(g, p), ctx.bound), None, None
 
 
 # ============================================================== elementwise
 class BoundFn(Function):
+    """LowerBound (upper=False) / UpperBound (upper=True), layers/bound.py:28-59."""
+
     @staticmethod
     def forward(ctx, x, bound, upper):
         _lib.require_device(x)
         x = _dense(x)
-        y = torch.empty_like(x)
-        _lib.check(_L().ic_bound_fwd(_lib.ptr(x), _n(x), float(bound), int(upper), _lib.ptr(y),
-                                     _lib.stream_of(x)), "bound_fwd")
-        ctx.conf = (float(bound), int(upper))
+        y = _lib.ops().bound_fwd(x, float(bound), bool(upper))
+        ctx.conf = (float(bound), bool(upper))
         ctx.save_for_backward(x)
         return y
 
@@ -292,20 +280,14 @@ class BoundFn(Function):
     def backward(ctx, g):
         (x,) = ctx.saved_tensors
         bound, upper = ctx.conf
-        g = _match(g, x)
-        gx = torch.empty_like(x)
-        _lib.check(_L().ic_bound_bwd(_lib.ptr(x), _lib.ptr(g), _n(x), bound, upper, _lib.ptr(gx),
-                                     _lib.stream_of(x)), "bound_bwd")
-        return gx, None, None
+        return _lib.ops().bound_bwd(x, _match(g, x), bound, upper), None, None
 
 
 class ReLUFn(Function):
     @staticmethod
     def forward(ctx, x):
         _lib.require_device(x)
-        x = _dense(x)
-        y = torch.empty_like(x)
-        _lib.check(_L().ic_relu_fwd(_lib.ptr(x), _n(x), _lib.ptr(y), _lib.stream_of(x)), "relu_fwd")
+        y = _lib.ops().relu_fwd(_dense(x))
         ctx.save_for_backward(y)
         return y
 
@@ -316,10 +298,7 @@ class ReLUFn(Function):
 
 
 def relu_bwd(y, g):
-    g = _match(g, y)
-    gx = torch.empty_like(y)
-    _lib.check(_L().ic_relu_bwd(_lib.ptr(y), _lib.ptr(g), _n(y), _lib.ptr(gx), _lib.stream_of(y)), "relu_bwd")
-    return gx
+    return _lib.ops().relu_bwd(y, _match(g, y))
 
 
 class AbsFn(Function):
@@ -327,18 +306,13 @@ class AbsFn(Function):
     def forward(ctx, x):
         _lib.require_device(x)
         x = _dense(x)
-        y = torch.empty_like(x)
-        _lib.check(_L().ic_abs_fwd(_lib.ptr(x), _n(x), _lib.ptr(y), _lib.stream_of(x)), "abs_fwd")
         ctx.save_for_backward(x)
-        return y
+        return _lib.ops().abs_fwd(x)
 
     @staticmethod
     def backward(ctx, g):
         (x,) = ctx.saved_tensors
-        g = _match(g, x)
-        gx = torch.empty_like(x)
-        _lib.check(_L().ic_abs_bwd(_lib.ptr(x), _lib.ptr(g), _n(x), _lib.ptr(gx), _lib.stream_of(x)), "abs_bwd")
-        return gx
+        return _lib.ops().abs_bwd(x, _match(g, x))
 
 
 class ExpClampFn(Function):
@@ -347,11 +321,7 @@ class ExpClampFn(Function):
     @staticmethod
     def forward(ctx, v, lo, hi):
         _lib.require_device(v)
-        v = _dense(v)
-        s = torch.empty_like(v)
-        e = torch.empty_like(v)
-        _lib.check(_L().ic_exp_clamp_fwd(_lib.ptr(v), _n(v), float(lo), float(hi), _lib.ptr(s), _lib.ptr(e),
-                                         _lib.stream_of(v)), "exp_clamp_fwd")
+        s, e = _lib.ops().exp_clamp_fwd(_dense(v), float(lo), float(hi))
         ctx.conf = (float(lo), float(hi))
         ctx.save_for_backward(e)
         return s
@@ -360,11 +330,7 @@ class ExpClampFn(Function):
     def backward(ctx, g):
         (e,) = ctx.saved_tensors
         lo, hi = ctx.conf
-        g = _match(g, e)
-        gv = torch.empty_like(e)
-        _lib.check(_L().ic_exp_clamp_bwd(_lib.ptr(e), _lib.ptr(g), _n(e), lo, hi, _lib.ptr(gv),
-                                         _lib.stream_of(e)), "exp_clamp_bwd")
-        return gv, None, None
+        return _lib.ops().exp_clamp_bwd(e, _match(g, e), lo, hi), None, None
 
 
 # ============================================================== losses
@@ -375,23 +341,13 @@ class CELossFn(Function):
     def forward(ctx, p):
         _lib.require_device(p)
         p = _dense(p)
-        out = torch.empty((), device=p.device, dtype=torch.float32)
-        L = _L()
-        nb = L.ic_reduce_ws(p.numel())
-        buf = _ws(nb, p.device)
-        _lib.check(L.ic_ce_loss_fwd(_lib.ptr(p), _n(p), _lib.ptr(out), _lib.ptr(buf), nb, _lib.stream_of(p)),
-                   "ce_loss_fwd")
         ctx.save_for_backward(p)
-        return out
+        return _lib.ops().ce_loss_fwd(p)
 
     @staticmethod
     def backward(ctx, g):
         (p,) = ctx.saved_tensors
-        g = g.contiguous()
-        gp = torch.empty_like(p)
-        _lib.check(_L().ic_ce_loss_bwd(_lib.ptr(p), _lib.ptr(g), _n(p), _lib.ptr(gp), _lib.stream_of(p)),
-                   "ce_loss_bwd")
-        return gp
+        return _lib.ops().ce_loss_bwd(p, g)
 
 
 class MSEFn(Function):
@@ -402,24 +358,14 @@ class MSEFn(Function):
         _lib.require_device(a, b)
         a = _dense(a)
         b = _match(b, a)
-        out = torch.empty((), device=a.device, dtype=torch.float32)
-        L = _L()
-        nb = L.ic_reduce_ws(a.numel())
-        buf = _ws(nb, a.device)
-        _lib.check(L.ic_mse_fwd(_lib.ptr(a), _lib.ptr(b), _n(a), _lib.ptr(out), _lib.ptr(buf), nb,
-                                _lib.stream_of(a)), "mse_fwd")
         ctx.save_for_backward(a, b)
-        return out
+        return _lib.ops().mse_fwd(a, b)
 
     @staticmethod
     def backward(ctx, g):
         a, b = ctx.saved_tensors
-        g = g.contiguous()
-        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
-        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
-        _lib.check(_L().ic_mse_bwd(_lib.ptr(a), _lib.ptr(b), _lib.ptr(g), _n(a), _lib.ptr(ga), _lib.ptr(gb),
-                                   _lib.stream_of(a)), "mse_bwd")
-        return ga, gb
+        ga, gb = _lib.ops().mse_bwd(a, b, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return (ga if ctx.needs_input_grad[0] else None), (gb if ctx.needs_input_grad[1] else None)
 
 
 # ============================================================== entropy models
@@ -432,6 +378,15 @@ def _from_last(t):
     return t.movedim(-1, 1)
 
 
+def _noise_arg(z, mode, u, last=False):
+    """The `u` operand of the quantizers: injected U[0,1) draws (mode 0, laid out like the
+    operand), the device Philox state (mode 3) or nothing."""
+    if u is None or mode == 3:
+        return u
+    u = u.to(z.dtype)
+    return _to_last(u) if last else _match(u, z)
+
+
 class FactorizedFn(Function):
     """EntropyModel._quantize + _prob_mass (entropy_model.py:216-269).
     Returns (q, p) in the input's logical (N, C, *) shape."""
@@ -439,18 +394,11 @@ class FactorizedFn(Function):
     @staticmethod
     def forward(ctx, z, mode, u, seed, offset, *params):
         _lib.require_device(z, None if mode == 3 else u, *params)
-        L = _L()
         C = z.shape[1]
         zl = _to_last(z)
-        # mode 3: `u` is the device {seed, base} state of the Philox stream
-        ul = u if (u is None or mode == 3) else _to_last(u.to(z.dtype))
-        q = torch.empty_like(zl)
-        p = torch.empty_like(zl)
         prm = [t.contiguous() for t in params]
-        cp = _lib.ICFactParams(*[ctypes.c_void_p(t.data_ptr()) for t in prm])
-        _lib.check(L.ic_factorized_fwd(_lib.ptr(zl), _n(zl), C, ctypes.byref(cp), int(mode), _lib.ptr(ul),
-                                       ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset), _lib.ptr(q),
-                                       _lib.ptr(p), _lib.stream_of(z)), "factorized_fwd")
+        q, p = _lib.ops().factorized_fwd(zl, C, prm, int(mode), _noise_arg(zl, mode, u, last=True), int(seed),
+                                         int(offset))
         ctx.mode = int(mode)
         ctx.C = C
         ctx.save_for_backward(q, *prm)
@@ -459,43 +407,17 @@ class FactorizedFn(Function):
     @staticmethod
     def backward(ctx, gq, gp):
         q, *prm = ctx.saved_tensors
-        L = _L()
-        gql = None if gq is None else _to_last(gq)
+        gql = None if (gq is None or ctx.mode == 1) else _to_last(gq)
         gpl = None if gp is None else _to_last(gp)
-        dz = torch.empty_like(q)
-        grads = [torch.empty_like(t) for t in prm]
-        cp = _lib.ICFactParams(*[ctypes.c_void_p(t.data_ptr()) for t in prm])
-        cg = _lib.ICFactGrads(*[ctypes.c_void_p(t.data_ptr()) for t in grads])
-        _lib.check(L.ic_factorized_bwd(_lib.ptr(q), _n(q), ctx.C, ctypes.byref(cp),
-                                       None if ctx.mode == 1 else _lib.ptr(gql), _lib.ptr(gpl), _lib.ptr(dz),
-                                       ctypes.byref(cg), _lib.stream_of(q)), "factorized_bwd")
+        dz, grads = _lib.ops().factorized_bwd(q, ctx.C, prm, gql, gpl)
         if ctx.mode == 1:  # torch.round has zero gradient
             dz.zero_()
         return (_from_last(dz), None, None, None, None, *grads)
 
 
-def _fact_net(dims, params):
-    """ic_fact_net for CDF layers of widths `dims` (1, DIMS..., 1) and their flat params
-    [w0, b0, f0, w1, b1, f1, ..., w_last, b_last] (CDFEstimator.flat_params order)."""
-    net = _lib.ICFactNet()
-    L = len(dims) - 1
-    net.nlayers = L
-    for i, d in enumerate(dims):
-        net.dims[i] = int(d)
-    k = 0
-    for layer in range(L):
-        net.w[layer] = params[k].data_ptr()
-        net.b[layer] = params[k + 1].data_ptr()
-        k += 2
-        if layer < L - 1:
-            net.f[layer] = params[k].data_ptr()
-            k += 1
-    return net
-
-
 class FactorizedNetFn(Function):
     """EntropyModel with any CDF MLP widths (cfg DIMS) and any BIN (entropy_model.py:88-99,
-    :198, :229-232, :259-269) on the generic kernels (ic_factorized_*_net)."""
+    :198, :229-232, :259-269) on the generic kernels (torch.ops.imgcomp.factorized_net_*)."""
 
     @staticmethod
     def forward(ctx, z, mode, u, seed, offset, dims, bin_, *params):
@@ -505,14 +427,9 @@ class FactorizedNetFn(Function):
                                       f"layers of width <= {_lib.FACT_MAXW}")
         C = z.shape[1]
         zl = _to_last(z)
-        ul = u if (u is None or mode == 3) else _to_last(u.to(z.dtype))
-        q = torch.empty_like(zl)
-        p = torch.empty_like(zl)
         prm = [t.contiguous() for t in params]
-        net = _fact_net(dims, prm)
-        _lib.check(_L().ic_factorized_fwd_net(_lib.ptr(zl), _n(zl), C, ctypes.byref(net), float(bin_), int(mode),
-                                              _lib.ptr(ul), ctypes.c_ulonglong(seed), ctypes.c_ulonglong(offset),
-                                              _lib.ptr(q), _lib.ptr(p), _lib.stream_of(z)), "factorized_fwd_net")
+        q, p = _lib.ops().factorized_net_fwd(zl, C, list(dims), float(bin_), prm, int(mode),
+                                             _noise_arg(zl, mode, u, last=True), int(seed), int(offset))
         ctx.conf = (int(mode), C, tuple(dims), float(bin_))
         ctx.save_for_backward(q, *prm)
         return _from_last(q), _from_last(p)
@@ -521,23 +438,9 @@ class FactorizedNetFn(Function):
     def backward(ctx, gq, gp):
         q, *prm = ctx.saved_tensors
         mode, C, dims, bin_ = ctx.conf
-        gql = None if gq is None else _to_last(gq)
+        gql = None if (gq is None or mode == 1) else _to_last(gq)
         gpl = None if gp is None else _to_last(gp)
-        dz = torch.empty_like(q)
-        grads = [torch.empty_like(t) for t in prm]
-        net = _fact_net(dims, prm)
-        g = _lib.ICFactNetGrads()
-        k = 0
-        for layer in range(len(dims) - 1):
-            g.w[layer] = grads[k].data_ptr()
-            g.b[layer] = grads[k + 1].data_ptr()
-            k += 2
-            if layer < len(dims) - 2:
-                g.f[layer] = grads[k].data_ptr()
-                k += 1
-        _lib.check(_L().ic_factorized_bwd_net(_lib.ptr(q), _n(q), C, ctypes.byref(net), bin_,
-                                              None if mode == 1 else _lib.ptr(gql), _lib.ptr(gpl), _lib.ptr(dz),
-                                              ctypes.byref(g), _lib.stream_of(q)), "factorized_bwd_net")
+        dz, grads = _lib.ops().factorized_net_bwd(q, C, list(dims), bin_, prm, gql, gpl)
         if mode == 1:  # torch.round has zero gradient
             dz.zero_()
         return (_from_last(dz), None, None, None, None, None, None, *grads)
@@ -549,19 +452,12 @@ class ConditionalFn(Function):
     @staticmethod
     def forward(ctx, y, scale, mean, kind, mode, u, seed, offset, bin_=1.0):
         _lib.require_device(y, scale, mean, None if mode == 3 else u)
-        L = _L()
         y = _dense(y)
         scale = _match(scale, y)
         if mean is not None:
             mean = _match(mean, y)
-        if u is not None and mode != 3:  # mode 3: `u` is the Philox device state
-            u = _match(u.to(y.dtype), y)
-        q = torch.empty_like(y)
-        p = torch.empty_like(y)
-        _lib.check(L.ic_conditional_fwd_bin(_lib.ptr(y), _lib.ptr(scale), _lib.ptr(mean), _n(y), int(kind),
-                                            int(mode), _lib.ptr(u), ctypes.c_ulonglong(seed),
-                                            ctypes.c_ulonglong(offset), float(bin_), _lib.ptr(q), _lib.ptr(p),
-                                            _lib.stream_of(y)), "conditional_fwd")
+        q, p = _lib.ops().conditional_fwd(y, scale, mean, int(kind), int(mode), _noise_arg(y, mode, u), int(seed),
+                                          int(offset), float(bin_))
         ctx.conf = (int(kind), int(mode), mean is not None, float(bin_))
         ctx.save_for_backward(q, scale, mean)
         return q, p
@@ -570,38 +466,28 @@ class ConditionalFn(Function):
     def backward(ctx, gq, gp):
         q, scale, mean = ctx.saved_tensors
         kind, mode, has_mean, bin_ = ctx.conf
-        L = _L()
         gq = None if gq is None else _match(gq, q)
         gp = None if gp is None else _match(gp, q)
-        dy = torch.empty_like(q) if ctx.needs_input_grad[0] else None
-        ds = torch.empty_like(q) if ctx.needs_input_grad[1] else None
-        dm = torch.empty_like(q) if (has_mean and ctx.needs_input_grad[2]) else None
-        _lib.check(L.ic_conditional_bwd_bin(_lib.ptr(q), _lib.ptr(scale), _lib.ptr(mean), _n(q), kind, bin_,
-                                            _lib.ptr(gq), _lib.ptr(gp), _lib.ptr(dy), _lib.ptr(ds), _lib.ptr(dm),
-                                            _lib.stream_of(q)), "conditional_bwd")
+        need = ctx.needs_input_grad
+        dy, ds, dm = _lib.ops().conditional_bwd(q, scale, mean, kind, bin_, gq, gp, need[0], need[1],
+                                                has_mean and need[2])
+        dy = dy if need[0] else None
         if mode == 1 and dy is not None:  # round: zero gradient through q
-            if gp is None:
-                dy.zero_()
-            else:
-                dy.zero_()
-        return dy, ds, dm, None, None, None, None, None, None
+            dy.zero_()
+        return (dy, ds if need[1] else None, dm if (has_mean and need[2]) else None,
+                None, None, None, None, None, None)
 
 
 class QuantizeFn(Function):
     """SymmetricConditionalModel._quantize alone (entropy_model.py:319-336): y + (u - bin/2) in
     training (straight-through: dq/dy = 1), round(y) in evaluation (zero gradient).  The same
-    draws, element for element, as ConditionalFn's quantization (ic_quantize)."""
+    draws, element for element, as ConditionalFn's quantization (torch.ops.imgcomp.quantize)."""
 
     @staticmethod
     def forward(ctx, y, mode, u, seed, offset, bin_):
         _lib.require_device(y, None if mode == 3 else u)
         y = _dense(y)
-        if u is not None and mode != 3:
-            u = _match(u.to(y.dtype), y)
-        q = torch.empty_like(y)
-        _lib.check(_L().ic_quantize(_lib.ptr(y), _n(y), int(mode), _lib.ptr(u), ctypes.c_ulonglong(seed),
-                                    ctypes.c_ulonglong(offset), float(bin_), _lib.ptr(q), _lib.stream_of(y)),
-                   "quantize")
+        q = _lib.ops().quantize(y, int(mode), _noise_arg(y, mode, u), int(seed), int(offset), float(bin_))
         ctx.mode = int(mode)
         return q
 
@@ -664,21 +550,14 @@ class SqDiffFn(Function):
         _lib.require_device(a, b)
         a = _dense(a)
         b = _match(b, a)
-        out = torch.empty_like(a)
-        _lib.check(_L().ic_sqdiff_fwd(_lib.ptr(a), _lib.ptr(b), _n(a), _lib.ptr(out), _lib.stream_of(a)),
-                   "sqdiff_fwd")
         ctx.save_for_backward(a, b)
-        return out
+        return _lib.ops().sqdiff_fwd(a, b)
 
     @staticmethod
     def backward(ctx, g):
         a, b = ctx.saved_tensors
-        g = _match(g, a)
-        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
-        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
-        _lib.check(_L().ic_sqdiff_bwd(_lib.ptr(a), _lib.ptr(b), _lib.ptr(g), _n(a), _lib.ptr(ga), _lib.ptr(gb),
-                                      _lib.stream_of(a)), "sqdiff_bwd")
-        return ga, gb
+        ga, gb = _lib.ops().sqdiff_bwd(a, b, _match(g, a), ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return (ga if ctx.needs_input_grad[0] else None), (gb if ctx.needs_input_grad[1] else None)
 
 
 class MSSSIMFn(Function):
@@ -687,43 +566,22 @@ class MSSSIMFn(Function):
     @staticmethod
     def forward(ctx, a, b, conf):
         _lib.require_device(a, b)
-        L = _L()
-        a = a.contiguous()
-        b = b.contiguous()
-        N, C, H, W = a.shape
         (nlev, fs, sigma, max_val, log_scale, single, k1, k2, eps, weights) = conf
-        sb = L.ic_msssim_state_bytes(N, C, H, W, nlev, fs)
-        if sb == 0:
-            raise RuntimeError(f"ms-ssim: image {H}x{W} too small for {nlev} levels of a {fs}x{fs} window")
-        state = torch.empty(sb // 4, device=a.device, dtype=torch.float32)
-        nb = L.ic_msssim_ws(N, C, H, W, nlev, fs)
-        buf = _ws(nb, a.device)
-        wts = (ctypes.c_float * nlev)(*weights)
-        out = torch.empty((N,) if (single and log_scale) else (), device=a.device, dtype=torch.float32)
-        _lib.check(L.ic_msssim_fwd(_lib.ptr(a), _lib.ptr(b), N, C, H, W, nlev, fs, sigma, max_val, int(log_scale),
-                                   int(single), k1, k2, eps, ctypes.cast(wts, ctypes.c_void_p), _lib.ptr(out),
-                                   _lib.ptr(state), _lib.ptr(buf), nb, _lib.stream_of(a)), "msssim_fwd")
+        out, state = _lib.ops().msssim_fwd(a, b, nlev, fs, sigma, max_val, bool(log_scale), int(single), k1, k2, eps,
+                                           list(weights))
         ctx.conf = conf
-        ctx.shape = (N, C, H, W)
+        ctx.shape = tuple(a.shape)
         ctx.save_for_backward(state)
         return out
 
     @staticmethod
     def backward(ctx, g):
         (state,) = ctx.saved_tensors
-        L = _L()
-        N, C, H, W = ctx.shape
         (nlev, fs, sigma, max_val, log_scale, single, k1, k2, eps, weights) = ctx.conf
-        g = g.contiguous()
-        ga = torch.empty((N, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
-        gb = torch.empty((N, C, H, W), device=g.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
-        nb = L.ic_msssim_ws(N, C, H, W, nlev, fs)
-        buf = _ws(nb, g.device)
-        wts = (ctypes.c_float * nlev)(*weights)
-        _lib.check(L.ic_msssim_bwd(N, C, H, W, nlev, fs, sigma, max_val, int(log_scale), int(single), k1, k2, eps,
-                                   ctypes.cast(wts, ctypes.c_void_p), _lib.ptr(g), _lib.ptr(state), _lib.ptr(ga),
-                                   _lib.ptr(gb), _lib.ptr(buf), nb, _lib.stream_of(g)), "msssim_bwd")
-        return ga, gb, None
+        need = ctx.needs_input_grad
+        ga, gb = _lib.ops().msssim_bwd(g, state, list(ctx.shape), nlev, fs, sigma, max_val, bool(log_scale),
+                                       int(single), k1, k2, eps, list(weights), need[0], need[1])
+        return (ga if need[0] else None), (gb if need[1] else None), None
 
 
 def msssim(img1, img2, mod, weights, single_scale):

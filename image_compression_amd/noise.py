@@ -14,7 +14,13 @@ step's total with a kernel (ic_philox_advance).  Because the advance is a
 kernel rather than a changed launch argument, a training step captured into a
 hipGraph (image_compression_amd.step) replays with fresh noise every time.
 The seed is drawn once from torch's default CPU generator (so
-`torch.manual_seed` makes runs reproducible).
+`torch.manual_seed` makes runs reproducible).  Under data parallelism every
+rank seeds its CPU generator alike, so the rank is folded into the Philox key
+(`rank_key`): rank r > 0 draws from key splitmix64(seed, r), independent of
+every other rank's stream, and rank 0 keeps the single-process key.  The
+reference draws `torch.rand_like` over the batch it holds (one process), so
+every image there gets its own noise; without the fold, image i of every rank
+would share one noise tensor.
 
 For bit-level parity with the reference, exact uniform draws can be injected:
 
@@ -48,14 +54,43 @@ def _key(device):
     return (d.type, d.index if d.index is not None else torch.cuda.current_device())
 
 
+_MASK62 = (1 << 62) - 1
+
+
+def _splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def rank_key(seed, rank):
+    """The Philox key of data-parallel rank `rank` for the shared seed `seed`: the seed
+    itself on rank 0, a splitmix64 hash of (seed, rank) elsewhere (62 bits, like the seed)."""
+    if rank == 0:
+        return int(seed)
+    return _splitmix64(_splitmix64(int(seed)) ^ int(rank)) & _MASK62
+
+
+def _dist_rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def process_key(seed):
+    """This process's Philox key for the shared seed (rank_key of its data-parallel rank)."""
+    return rank_key(seed, _dist_rank())
+
+
 def device_state(device):
-    """The {seed, base} tensor of `device` (created on first use)."""
+    """The {seed, base} tensor of `device` (created on first use; the key folds in this
+    process's data-parallel rank, see rank_key)."""
     s = _st()
     k = _key(device)
     if k not in s.dev:
         if s.seed is None:
             s.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        s.dev[k] = torch.tensor([s.seed, 0], dtype=torch.int64, device=torch.device(*k))
+        s.dev[k] = torch.tensor([process_key(s.seed), 0], dtype=torch.int64, device=torch.device(*k))
         s.offset[k] = 0
     return s.dev[k]
 
@@ -78,9 +113,7 @@ def begin_step(device):
     k = _key(device)
     n = s.offset.get(k, 0)
     if n:
-        _lib.check(_lib.load().ic_philox_advance(_lib.ptr(s.dev[k]), _lib.c_ull(n),
-                                                 _lib.c_void(torch.cuda.current_stream(s.dev[k].device).cuda_stream)),
-                   "philox_advance")
+        _lib.ops().philox_advance(s.dev[k], int(n))
         s.offset[k] = 0
 
 

@@ -64,16 +64,27 @@ class TrainStep:
         losses["total_loss"].backward()
         return losses
 
+    def _eager(self):
+        losses = self._step()
+        return {k: v.detach() for k, v in losses.items()}
+
     def _capture(self, warmup):
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream(self.x.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):       # allocator pools warm, kernels loaded
-                self._step()
+                self._eager()
         torch.cuda.current_stream(self.x.device).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.losses = self._step()
+            losses = self._step()
+        # keep the graph's static loss outputs, not the autograd graph behind them: that graph
+        # holds the parameters' AccumulateGrad nodes made on the capture stream, and a later
+        # eager step through those nodes would accumulate its gradients on the capture stream
+        # (torch: "AccumulateGrad node's stream does not match") -- a cross-stream use the
+        # caching allocator is not told about
+        self.losses = {k: v.detach() for k, v in losses.items()}
+        del losses
 
     def __call__(self, x=None):
         """Run one step; returns the loss dict (0-dim device tensors; with a
@@ -84,9 +95,10 @@ class TrainStep:
             self.graph.replay()
             losses = self.losses
         else:
-            losses = self._step()
+            losses = self._eager()
         if self.flat_grad is not None and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.AVG)
+            from .distributed import all_reduce_mean_
+            all_reduce_mean_(self.flat_grad)
         return losses
 
     def grads(self):

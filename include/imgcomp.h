@@ -135,10 +135,7 @@ size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math);
 int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
                   int math, void* ws, size_t ws_bytes, void* stream);
 /* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three bf16
- * terms on the bf16 MFMA), dx on the fp32 MFMA; IC_MATH_SPLIT | IC_MATH_GDN_BWD_FULL_SPLIT runs dx in split
- * arithmetic too (12-wave kernel; measured no faster: register-bound at 16-pixel tiles).  Other shapes stay
- * on the fp32 MFMA. */
-#define IC_MATH_GDN_BWD_FULL_SPLIT 8
+ * terms on the bf16 MFMA), dx on the fp32 MFMA.  Other shapes stay on the fp32 MFMA. */
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
 /* ic_gdn_bwd_ex plus dxsum[c] = sum over all pixels of dx[.,c,.,.] (C floats): the bias gradient of
@@ -252,7 +249,11 @@ int ic_philox_advance(unsigned long long* state, unsigned long long n, void* str
  *      mode: 0 = noise with given u (u in [0,1), y = z + (u - 0.5)), 1 = round,
  *            2 = noise from Philox(seed, offset),
  *            3 = noise from Philox(state[0], state[1] + offset) with `u` pointing to the
- *                device state {seed, base} of ic_philox_advance (`seed` ignored) */
+ *                device state {seed, base} of ic_philox_advance (`seed` ignored).
+ *      Modes 2 and 3 take a 4-aligned offset only (IC_ERR_ARG otherwise) and mode 3 a
+ *      4-aligned state[1] (ic_philox_advance keeps it so; a caller writing the state
+ *      itself must too): every draw is then whole Philox blocks and every quantizer
+ *      kernel maps element i to the same counter */
 typedef struct ic_fact_params {
   const float *w0, *b0, *f0, *w1, *b1, *f1, *w2, *b2, *f2, *w3, *b3;
 } ic_fact_params;

@@ -209,3 +209,102 @@ def test_torch_ops_registered_with_shape_kernels():
     for name in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad", "conv_transpose2d_fwd", "conv_transpose2d_dgrad",
                  "conv_transpose2d_wgrad", "gdn_fwd", "gdn_bwd"):
         assert hasattr(ops, name), name
+
+
+def _meta(*shape, cl=False, dtype=torch.float32):
+    t = torch.empty(*shape, device="meta", dtype=dtype)
+    return t.contiguous(memory_format=torch.channels_last) if cl else t
+
+
+# every torch.ops.imgcomp op -> a call on meta tensors and the output shapes it must infer
+def _meta_cases():
+    x = _meta(2, 192, 16, 16, cl=True)
+    img = _meta(2, 3, 64, 64)
+    zl = _meta(2, 4, 4, 192)
+    fact = [_meta(192 * n) for n in (3, 3, 3, 9, 3, 3, 9, 3, 3, 3, 1)]
+    net = [_meta(192 * n) for n in (2, 2, 2, 8, 4, 4, 4, 1)]   # DIMS [2, 4]: 1 -> 2 -> 4 -> 1
+    st = _meta(2, dtype=torch.int64)
+    w = [.0448, .2856, .3001, .2363, .1333]
+    s = x.shape
+    return {
+        "nonneg_fwd": (lambda o: o.nonneg_fwd(_meta(192, 192), 0.0, 2 ** -36), [(192, 192)]),
+        "nonneg_bwd": (lambda o: o.nonneg_bwd(_meta(192), _meta(192), 0.0), [(192,)]),
+        "bound_fwd": (lambda o: o.bound_fwd(img, 1.0, True), [img.shape]),
+        "bound_bwd": (lambda o: o.bound_bwd(img, img, 0.0, False), [img.shape]),
+        "relu_fwd": (lambda o: o.relu_fwd(x), [s]),
+        "relu_bwd": (lambda o: o.relu_bwd(x, x), [s]),
+        "abs_fwd": (lambda o: o.abs_fwd(x), [s]),
+        "abs_bwd": (lambda o: o.abs_bwd(x, x), [s]),
+        "exp_clamp_fwd": (lambda o: o.exp_clamp_fwd(x, 1e-10, 1e10), [s, s]),
+        "exp_clamp_bwd": (lambda o: o.exp_clamp_bwd(x, x, 1e-10, 1e10), [s]),
+        "ce_loss_fwd": (lambda o: o.ce_loss_fwd(x), [()]),
+        "ce_loss_bwd": (lambda o: o.ce_loss_bwd(x, _meta(())), [s]),
+        "mse_fwd": (lambda o: o.mse_fwd(img, img), [()]),
+        "mse_bwd": (lambda o: o.mse_bwd(img, img, _meta(()), True, False), [img.shape, (0,)]),
+        "sqdiff_fwd": (lambda o: o.sqdiff_fwd(img, img), [img.shape]),
+        "sqdiff_bwd": (lambda o: o.sqdiff_bwd(img, img, img, True, True), [img.shape, img.shape]),
+        "factorized_fwd": (lambda o: o.factorized_fwd(zl, 192, fact, 3, st, 0, 0), [zl.shape, zl.shape]),
+        "factorized_bwd": (lambda o: (lambda r: (r[0], *r[1]))(o.factorized_bwd(zl, 192, fact, zl, zl)),
+                           [zl.shape] + [t.shape for t in fact]),
+        "factorized_net_fwd": (lambda o: o.factorized_net_fwd(zl, 192, [1, 2, 4, 1], 2.0, net, 1, None, 0, 0),
+                               [zl.shape, zl.shape]),
+        "factorized_net_bwd": (lambda o: (lambda r: (r[0], *r[1]))(o.factorized_net_bwd(zl, 192, [1, 2, 4, 1], 2.0,
+                                                                                          net, None, zl)),
+                               [zl.shape] + [t.shape for t in net]),
+        "quantize": (lambda o: o.quantize(x, 3, st, 0, 0, 1.0), [s]),
+        "conditional_fwd": (lambda o: o.conditional_fwd(x, x, None, 0, 4, None, 0, 0, 1.0), [s, s]),
+        "conditional_bwd": (lambda o: o.conditional_bwd(x, x, None, 1, 1.0, x, x, True, True, True), [s, s, (0,)]),
+        "philox_advance": (lambda o: (o.philox_advance(st, 100), ())[1], []),
+        "msssim_fwd": (lambda o: o.msssim_fwd(_meta(2, 3, 256, 256), _meta(2, 3, 256, 256), 5, 11, 1.5, 255.0,
+                                              True, 0, 0.01, 0.03, 1e-5, w), [(), None]),
+        "msssim_bwd": (lambda o: o.msssim_bwd(_meta(()), _meta(1000), [2, 3, 256, 256], 5, 11, 1.5, 255.0, True, 0,
+                                              0.01, 0.03, 1e-5, w, True, False), [(2, 3, 256, 256), (0,)]),
+        "conv2d_fwd": (lambda o: o.conv2d_fwd(x, _meta(192, 192, 5, 5), None, 2, 2, 0, 2), [(2, 192, 8, 8)]),
+        "conv2d_dgrad": (lambda o: o.conv2d_dgrad(_meta(2, 192, 8, 8, cl=True), _meta(192, 192, 5, 5), x, 2, 2, 2),
+                         [s]),
+        "conv2d_wgrad": (lambda o: o.conv2d_wgrad(x, _meta(2, 192, 8, 8, cl=True), _meta(192, 192, 5, 5), 2, 2, True,
+                                                  2), [(192, 192, 5, 5), (192,)]),
+        "conv_transpose2d_fwd": (lambda o: o.conv_transpose2d_fwd(_meta(2, 192, 8, 8, cl=True), _meta(192, 192, 5, 5),
+                                                                  None, 2, 2, 1, 0, 2), [s]),
+        "conv_transpose2d_dgrad": (lambda o: o.conv_transpose2d_dgrad(x, _meta(192, 192, 5, 5),
+                                                                      _meta(2, 192, 8, 8, cl=True), 2, 2, 2),
+                                   [(2, 192, 8, 8)]),
+        "conv_transpose2d_wgrad": (lambda o: o.conv_transpose2d_wgrad(_meta(2, 192, 8, 8, cl=True), x,
+                                                                      _meta(192, 192, 5, 5), 2, 2, True, 2),
+                                   [(192, 192, 5, 5), (192,)]),
+        "gdn_fwd": (lambda o: o.gdn_fwd(x, _meta(192, 192), _meta(192), False, 2), [s, s]),
+        "gdn_bwd": (lambda o: o.gdn_bwd(x, x, x, _meta(192, 192), False, 2), [s, (192, 192), (192,)]),
+        "gdn_bwd_sum": (lambda o: o.gdn_bwd_sum(x, x, x, _meta(192, 192), False, 2),
+                        [s, (192, 192), (192,), (192,)]),
+    }
+
+
+def test_every_registered_op_has_a_meta_kernel():
+    """every launcher the training step calls is a torch.ops.imgcomp operator with a
+    shape (Meta) kernel -- convolutions, GDN, elementwise bounds / ReLU / abs / exp-clamp, the
+    factorized and conditional entropy models, the quantizer, the losses (CE, MSE, MS-SSIM) and
+    the noise-state advance.  Each is called on meta tensors here (no GPU)."""
+    from image_compression_amd import _lib
+    ops = _lib.ops()
+    cases = _meta_cases()
+    registered = {name.split("::")[1] for name in torch._C._dispatch_get_all_op_names() if name.startswith("imgcomp::")}
+    assert registered == set(cases), sorted(registered ^ set(cases))
+    for name, (call, shapes) in cases.items():
+        out = call(ops)
+        out = out if isinstance(out, tuple) else (out,)
+        assert len(out) == len(shapes), name
+        for t, shp in zip(out, shapes):
+            assert t.device.type == "meta", name
+            if shp is not None:
+                assert tuple(t.shape) == tuple(shp), (name, tuple(t.shape), shp)
+
+
+def test_training_step_path_has_no_ctypes_call():
+    """functional.py (the autograd Functions of the training step) dispatches every launch
+    through torch.ops.imgcomp; the ctypes binding stays for the non-torch C ABI users."""
+    import inspect
+
+    from image_compression_amd import functional, noise
+    for mod in (functional, noise):
+        src = inspect.getsource(mod)
+        assert "ctypes" not in src and "_lib.load()" not in src and "_L()" not in src, mod.__name__

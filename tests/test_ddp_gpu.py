@@ -1,7 +1,11 @@
 """The data-parallel path with the HIP kernels: two ranks (gloo over GPU
 tensors, sharing the box's one GPU — the RCCL path needs one GPU per rank),
-each on half the batch under DistributedDataParallel, average to the
-single-process gradient of the whole batch (injected noise, fixed weights)."""
+each on half the batch, average to the single-process gradient of the whole
+batch (injected noise, fixed weights) -- under DistributedDataParallel (the
+single-stream step D.wrap selects) and through TrainStep's flat gradient
+buffer and one all-reduce (with the hyperprior side stream).  The ranks'
+training-noise keys differ (noise.rank_key).  Unmeasured on RCCL hardware:
+the box has one GPU."""
 import os
 import socket
 
@@ -34,9 +38,12 @@ def _worker(rank, world, port, outdir):
                       LOCAL_RANK=str(rank), IMGCOMP_DIST_BACKEND="gloo")
     from image_compression_amd import distributed as D
     from image_compression_amd import injected_noise, modelling
+    from image_compression_amd import noise
+    from image_compression_amd.step import TrainStep
     _, _, dev = D.setup()
     torch.manual_seed(0)
     model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev, bucket_cap_mb=4.0)
+    assert model.module.concurrent_hyperprior is False     # D.wrap decides the side stream under DDP
     x, uz, uy = (D.shard(t, rank, world).to(dev) for t in _inputs())
     for _ in range(2):       # DDP raises on the 2nd iteration if a parameter went unused
         model.zero_grad(set_to_none=True)
@@ -44,9 +51,25 @@ def _worker(rank, world, port, outdir):
             _, losses = model(x)
         losses["total_loss"].backward()
     torch.cuda.synchronize()
+    ddp_grads = {n: p.grad.detach().cpu() for n, p in model.module.named_parameters()}
+    # the hipGraph-capable step without DDP: gradients as views of one flat buffer, one
+    # all-reduce after the backward, hyperprior side stream on
+    torch.manual_seed(0)
+    m2 = modelling.build_model(_cfg()).to(dev).train()
+    assert m2.concurrent_hyperprior
+    st = TrainStep(m2, x, graph=False)
+    assert st.flat_grad is not None
+    with injected_noise([uz, uy]):
+        st(x)
+    torch.cuda.synchronize()
+    flat_grads = {n: p.grad.detach().cpu() for n, p in m2.named_parameters()}
+    # the training-noise keys of the two ranks (device state, rank folded in)
+    key = noise.device_state(dev)[0:1].clone()
+    keys = [torch.zeros_like(key) for _ in range(world)]
+    torch.distributed.all_gather(keys, key)
     if rank == 0:
-        torch.save({n: p.grad.detach().cpu() for n, p in model.module.named_parameters()},
-                   os.path.join(outdir, "g.pt"))
+        torch.save({"ddp": ddp_grads, "flat": flat_grads, "keys": [int(k) for k in keys],
+                    "seed": noise._st().seed}, os.path.join(outdir, "g.pt"))
     D.teardown()
 
 
@@ -57,12 +80,16 @@ def test_ddp_two_ranks_match_full_batch(tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
-    g = torch.load(os.path.join(tmp_path, "g.pt"), weights_only=True)
+    res = torch.load(os.path.join(tmp_path, "g.pt"), weights_only=True)
+    from image_compression_amd import noise
+    assert res["keys"] == [noise.rank_key(res["seed"], r) for r in range(2)] and res["keys"][0] != res["keys"][1]
     torch.manual_seed(0)
     model = modelling.build_model(_cfg()).cuda().train()
     x, uz, uy = (t.cuda() for t in _inputs())
     with injected_noise([uz, uy]):
         _, losses = model(x)
     losses["total_loss"].backward()
-    worst = max((rel_err(g[n], p.grad.cpu()), n) for n, p in model.named_parameters())
-    assert worst[0] < 1e-4, worst
+    for kind in ("ddp", "flat"):
+        g = res[kind]
+        worst = max((rel_err(g[n], p.grad.cpu()), n) for n, p in model.named_parameters())
+        assert worst[0] < 1e-4, (kind, worst)

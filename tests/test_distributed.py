@@ -117,3 +117,53 @@ def test_shard_and_single_rank_helpers():
     m = torch.nn.Linear(2, 2)
     assert D.wrap(m, torch.device("cpu")) is m          # no process group: no wrapper
     assert D.max_over_ranks(3.5, torch.device("cpu")) == 3.5
+
+
+def _key_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from image_compression_amd import distributed as D
+    from image_compression_amd import noise
+    D.setup("gloo", device_type="cpu")
+    torch.manual_seed(0)                       # every rank seeds alike, as bench.py does
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    keys = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    torch.distributed.all_gather(keys, torch.tensor([noise.process_key(seed)]))
+    if rank == 0:
+        torch.save({"seed": seed, "keys": [int(k) for k in keys]}, os.path.join(outdir, "keys.pt"))
+    D.teardown()
+
+
+def test_ranks_draw_independent_noise(tmp_path):
+    """Under data parallelism every rank seeds alike; the rank folded into the Philox key
+    gives each rank its own z / y draws (the reference's one process draws torch.rand_like
+    over its whole batch: no image shares noise with another, entropy_model.py:230,333)."""
+    import numpy as np
+
+    from image_compression_amd import noise
+    from oracle import philox
+    world = 4
+    mp.start_processes(_key_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = torch.load(os.path.join(tmp_path, "keys.pt"), weights_only=True)
+    seed, keys = res["seed"], res["keys"]
+    assert keys[0] == seed                                   # rank 0 keeps the single-process stream
+    assert keys == [noise.rank_key(seed, r) for r in range(world)]
+    assert len(set(keys)) == world and all(0 <= k < 2 ** 62 for k in keys)
+    # one C2-sized step per rank: z (32 x 192 x 4 x 4) then y (32 x 192 x 16 x 16), 4-aligned offsets
+    nz, ny = 32 * 192 * 16, 32 * 192 * 256
+    draws = [np.concatenate([philox.uniform(nz, k, 0), philox.uniform(ny, k, nz)]) for k in keys]
+    for a in range(world):
+        for b in range(a + 1, world):
+            same = int((draws[a] == draws[b]).sum())
+            # independent 24-bit uniforms coincide with probability 2^-24 per element
+            assert same <= 8, (a, b, same)
+            assert abs(float(np.corrcoef(draws[a], draws[b])[0, 1])) < 0.01
+
+
+def test_rank_key_is_a_fixed_function():
+    from image_compression_amd import noise
+    assert noise.rank_key(12345, 0) == 12345
+    assert noise.rank_key(12345, 1) == noise.rank_key(12345, 1) != noise.rank_key(12345, 2)
+    assert noise.rank_key(12345, 1) != noise.rank_key(12346, 1)
+    assert noise.process_key(777) == 777                     # no process group: rank 0

@@ -53,11 +53,12 @@ def _run(model, x, u_z, u_y, train):
         {k: v.detach().cpu().numpy() for k, v in losses.items()}
 
 
+@pytest.mark.parametrize("dtype", ["fp32_split", "fp32"])  # the default (benched) arithmetic and the fp32 MFMA
 @pytest.mark.parametrize("name", golden_names("small_"))
-def test_model_matches_reference_golden(name):
+def test_model_matches_reference_golden(name, dtype):
     from image_compression_amd import modelling
     meta, d = load_golden(name)
-    model = modelling.build_model(_cfg(meta["over"]))
+    model = modelling.build_model(_cfg(dict(meta["over"], **{"MODEL.COMPUTE_DTYPE": dtype})))
     sd = {k: torch.from_numpy(v) for k, v in params_of(d).items()}
     model.load_state_dict(sd, strict=True)
     model = model.to(DEV)

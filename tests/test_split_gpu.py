@@ -55,6 +55,8 @@ def _check(split, native, ref, name, ran=True):
 @pytest.mark.parametrize("n,cin,cout,h,w,k,s", [
     (2, 192, 192, 32, 32, 5, 2),     # g_a body layer
     (3, 192, 192, 20, 12, 5, 2),     # ragged, several images
+    (1, 192, 192, 30, 32, 5, 2),     # output 15x16: 16-wide rows, P = 240 = 32*7 + 16 (half a wgrad step)
+    (3, 192, 192, 30, 32, 5, 2),     # P = 720, odd row count over several images
     (2, 3, 192, 40, 72, 5, 2),       # g_a.0 edge: edge_conv / edge_wgrad (split wgrad), ragged unit
     (2, 192, 192, 16, 16, 3, 1),     # h_a.0
     (2, 320, 192, 8, 8, 5, 2),       # latent 320 reduction
@@ -186,7 +188,7 @@ def test_gdn_split_dgamma(n, h, w, inverse):
     gy = _r(*yr.shape, seed=13)
     yr.backward(gy.double())
     out = {}
-    for math in (2, 0, 2 | 8):   # split dgamma, fp32, split dx + dgamma (IC_MATH_GDN_BWD_FULL_SPLIT)
+    for math in (2, 0):   # split dgamma, fp32
         md = m.to(DEV)
         md.math = math
         md.zero_grad()
@@ -196,9 +198,6 @@ def test_gdn_split_dgamma(n, h, w, inverse):
     _check(out[2][1], out[0][1], gp.grad, "dgamma")
     assert_close(out[2][0], xr.grad, 1e-4, "dx")
     assert_close(out[2][2], bp.grad, 1e-4, "dbeta")
-    _check(out[10][1], out[0][1], gp.grad, "dgamma (full split)")
-    _check(out[10][0], out[0][0], xr.grad, "dx (full split)")
-    assert_close(out[10][2], bp.grad, 1e-4, "dbeta (full split)")
 
 
 # (8, 192, 67, 65): 1,089 32-pixel tiles, 4-5 per block of the pipelined split kernel, last one partial
