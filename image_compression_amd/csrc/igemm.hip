@@ -739,6 +739,198 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
 }
 
+// ------------------------------------------------------------------ split, A in registers
+// The split implicit GEMM with no LDS image of A: each wave gathers its own
+// 64 rows x 32 channels of the K chunk straight from global memory in the
+// 16x16x32 A-fragment layout (lane (r, g): row r, channels 8g .. 8g+7, two
+// 16-B loads per 16-row tile) and splits them in registers; the two waves of
+// a block that share those rows read the same lines, the second from L1.
+// Only B — the three pre-split weight planes, 36 KB per chunk at BN = 192 —
+// goes through LDS, by LDS-DMA (global_load_lds_dwordx4 from inline asm: no
+// VGPR staging, no ds_write), into two stages (72 KB, two blocks per CU),
+// with ONE barrier per chunk: at the top of chunk c every wave waits for its
+// own DMA of B(c) and its loads of A(c) (vmcnt(0)) and the barrier publishes
+// B(c) and retires every read of the stage that B(c+1) then overwrites.
+// Per chunk: barrier, split A(c) (32 values per lane), issue DMA B(c+1) and
+// the loads of A(c+1), then the 144 MFMAs of chunk c.  The MFMAs are the
+// same six products in the same order as ig_kernel_x3s, so the result is
+// bitwise that kernel's.  The DMA source addresses carry the B swizzle
+// (ig_swz): lane L of a DMA instruction lands in LDS slot L & 3 of row L >> 2
+// and fetches the logical 16-B chunk (L & 3) ^ ig_swz(row) of its row.
+#ifndef IG_X3R
+#define IG_X3R 0  // 1: 128-row split tiles on ig_kernel_x3r (measured 4 % slower than ig_kernel_x3s, r03b)
+#endif
+
+__device__ __attribute__((aligned(16))) float ig_zero_page8[8];
+
+// 16 B per lane, global -> LDS at byte offset lds + 16 * lane (wave-uniform lds)
+__device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
+  uint32_t save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+#ifndef IG_X3R_SGB
+#define IG_X3R_SGB 2  // ig_kernel_x3r: one A load per IG_X3R_SGB MFMAs at the top of the chunk's MFMAs
+#endif
+
+template <int BM, int BN, int WM, int WN, bool SQ>
+__global__ void __launch_bounds__(256, 2) ig_kernel_x3r(const IgDesc d) {
+  constexpr int NP = 3, LDB = 32;
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int BROWS = NP * BN;           // 64-B rows per B stage
+  constexpr int BSTAGE = BROWS * LDB;      // bf16 elements per stage
+  constexpr int NDMA = BROWS / 16 / 4;     // 1-KB DMA instructions per wave per chunk
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(BROWS % 64 == 0, "whole DMA instructions per wave");
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2 * BSTAGE];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int n0 = blockIdx.y * BN;
+  const int T = P.T;
+  const int nchunks = T * (d.Cin >> 5);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
+  const int r = lane & 15, g = lane >> 4;
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+
+  // A: this lane's rows m0 + wm*WM + 16 i + r
+  uint32_t a_off[TM];
+  int a_iy[TM], a_ix[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const uint32_t m = m0 + wm * WM + 16 * i + r;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[i] = ok ? (int)gy * d.stride : -0x40000000;  // invalid rows fail the bounds test
+    a_ix[i] = (int)gx * d.stride;
+    a_off[i] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[i] * xsh + (uint32_t)a_ix[i] * xsw + 8u * g;
+  }
+  const float* __restrict__ xg = d.x;
+
+  // B: DMA instruction j of this wave moves 64-B rows R = (w*NDMA + j)*16 + (lane >> 2)
+  // (plane R / BN, row R % BN), slot lane & 3 <- logical chunk (lane & 3) ^ ig_swz(row)
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  uint32_t b_src[NDMA];
+#pragma unroll
+  for (int j = 0; j < NDMA; ++j) {
+    const int R = (w * NDMA + j) * 16 + (lane >> 2);
+    const int q = R / BN, row = R - (R / BN) * BN;
+    b_src[j] = (uint32_t)(q * d.wplane) + (uint32_t)(n0 + row) * (uint32_t)d.Cin + 8u * ((lane & 3) ^ ig_swz(row));
+  }
+  // LDS byte offset of this wave's DMA rows in stage 0
+  const uint32_t lds_b = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) __bf16*)Bs + (uint32_t)(w * NDMA * 16 * LDB * 2));
+  const size_t tstride = (size_t)d.Npad * d.Cin;
+  auto dma_b = [&](int cc, int t, int stage) {
+    const __bf16* base = wpb + (size_t)t * tstride + cc * 32;
+    const uint32_t dst = lds_b + (uint32_t)(stage * BSTAGE * 2);
+#pragma unroll
+    for (int j = 0; j < NDMA; ++j) ig_glds16(base + b_src[j], dst + (uint32_t)(j * 16 * LDB * 2));
+  };
+
+  floatx4v raw[TM][2];
+  auto load_a = [&](int cc, int t) {
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      const float* src = in ? xg + (a_off[i] + toff) : ig_zero_page8;
+      raw[i][0] = *(const floatx4v*)src;
+      raw[i][1] = *(const floatx4v*)(src + 4);
+    }
+  };
+
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  // chunk c = (channel chunk cc, tap t): channel chunk outer, tap inner (as ig_kernel_x3s)
+  int cc = cb / T, t = cb - (cb / T) * T;
+  if (cb < ce) {
+    dma_b(cc, t, 0);
+    load_a(cc, t);
+  }
+  const int ch = 8 * (g ^ ig_swz(r));
+  for (int c = cb; c < ce; ++c) {
+    const int stage = (c - cb) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // split A(c): a[q][i] = plane q (hi, mid, lo) of rows 16 i + r, channels 8g .. 8g+7
+    bf16x8 a[NP][TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      bf16x4 h0, md0, l0, h1, md1, l1;
+      split3_bf16x4(SQ ? raw[i][0] * raw[i][0] : raw[i][0], h0, md0, l0);
+      split3_bf16x4(SQ ? raw[i][1] * raw[i][1] : raw[i][1], h1, md1, l1);
+      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[1][i] = __builtin_shufflevector(md0, md1, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    const bool more = c + 1 < ce;
+    const int cn = (t + 1 == T) ? cc + 1 : cc, tn = (t + 1 == T) ? 0 : t + 1;
+    if (more) dma_b(cn, tn, stage ^ 1);
+    // unconditional: the last chunk reloads itself (unused), so the loads share the MFMAs' block
+    load_a(more ? cn : cc, more ? tn : t);
+    const __bf16* Brd = Bs + stage * BSTAGE + (wn * WN + r) * LDB + ch;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+      }
+    }
+    if constexpr (IG_X3R_SGB > 0) {
+      // the next chunk's A loads at the top of this chunk's MFMAs (the compiler would sink them
+      // to the loop end, where the barrier's vmcnt(0) then waits out their whole latency)
+#pragma unroll
+      for (int k = 0; k < 2 * TM; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);            // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, IG_X3R_SGB, 0);   // MFMA
+      }
+    }
+    cc = cn;
+    t = tn;
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
+}
+
 // split-K reduction + epilogue: one thread per (row, channel)
 __global__ void ig_reduce_kernel(const IgDesc d) {
   const long long total = d.Mtot * d.Cout;
@@ -790,6 +982,13 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
       }
       return IC_ERR_ARG;
     case IC_KERNEL_IG_SPLIT:
+      if constexpr (BN % 64 == 0 && BM == 128) {
+        if (IG_X3R) {
+          if (sq) hipLaunchKernelGGL((ig_kernel_x3r<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
+          else hipLaunchKernelGGL((ig_kernel_x3r<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
+          break;
+        }
+      }
       if constexpr (BN % 64 == 0) {
         hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
         break;

@@ -246,10 +246,18 @@ void check_dense(const Tensor& t, const char* what) {
   TORCH_CHECK(t.is_non_overlapping_and_dense(), "imgcomp: ", what, " must be dense (non-overlapping) storage");
 }
 
+// same shape and the same strides on every dimension of extent > 1 (a size-1 dimension's
+// stride addresses nothing): element i of the dense storage is the same logical element in both
+bool same_layout(const Tensor& a, const Tensor& b) {
+  if (a.sizes() != b.sizes()) return false;
+  for (int64_t i = 0; i < a.dim(); ++i)
+    if (a.size(i) > 1 && a.stride(i) != b.stride(i)) return false;
+  return true;
+}
+
 void check_same_layout(const Tensor& a, const Tensor& b, const char* what) {
   check_dense(b, what);
-  TORCH_CHECK(a.sizes() == b.sizes() && a.strides() == b.strides(), "imgcomp: ", what,
-              " must have the shape and strides of its partner operand");
+  TORCH_CHECK(same_layout(a, b), "imgcomp: ", what, " must have the shape and strides of its partner operand");
 }
 
 Tensor like(const Tensor& t) { return at::empty_like(t, at::MemoryFormat::Preserve); }
