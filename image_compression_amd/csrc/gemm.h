@@ -32,6 +32,10 @@ struct IgPhase {
   long long m_off;  // row offset of this phase inside the split-K partial buffer
   FastDiv fd_hw, fd_w;  // divide by Hg*Wg and by Wg
   int dy[IC_MAXT], dx[IC_MAXT];
+  // halo tiles (ig_kernel_halo, set by ig_plan): a tile is hrows whole rows of the output grid;
+  // its input patch spans rows gy0*stride + hdy0 + [0, hph) and columns hdx0 + [0, hpw), stored
+  // with hpw_l pixels per row (stride 2: even columns, then odd ones from hpw2)
+  int hrows, hdy0, hdx0, hph, hpw, hpw2, hpw_l;
 };
 
 struct IgDesc {
@@ -58,6 +62,7 @@ struct IgDesc {
   int x3;            // fp32 by exact three-term bf16 split (fast path, Cin % 32 == 0); wp holds three
                      // bf16 planes [part][t][Npad][Cin], part p at wp + p * wplane (bf16 elements)
   long long wplane;
+  int halo;          // split tiles on ig_kernel_halo (set by ig_plan)
   IgPhase ph[IC_MAXPH];
 };
 

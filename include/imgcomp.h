@@ -184,6 +184,8 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
 #define IC_KERNEL_GDN_FUSED 16      /* gdn_fwd_fused_kernel / gdn_bwd_fused_kernel (fp32 dx) */
 #define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3s_kernel / gdn_bwd_fused_kernel with split dgamma */
 #define IC_KERNEL_GDN_GEMM 18       /* GDN on the implicit GEMM (+ wgrad kernel for dgamma) */
+#define IC_KERNEL_IG_SPLIT_HALO 19  /* ig_kernel_halo: split arithmetic, 128-row tiles, input patch staged once
+                                       per 16-channel chunk and shared by every tap */
 typedef struct ic_plan {
   int kernel;        /* IC_KERNEL_* of the main launch */
   int bm, bn;        /* block tile: output rows (pixels; weight-gradient: G channels) x columns */

@@ -50,7 +50,7 @@ def test_c2_conv_layer(math):
     y = IF.conv2d(xd, wd, b.to(DEV), 2, 2, math=math)
     gy = _r(*y.shape, seed=4).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split", 1: "ig_bf16"}[math]
+    kern = {2: "ig_split_halo", 1: "ig_bf16"}[math]  # split: the halo-reusing kernel at these shapes
     pf = _lib.plan("conv2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
@@ -84,7 +84,7 @@ def test_c2_tconv_layer(math):
     y = IF.conv_transpose2d(xd, wd, None, 2, 2, 1, math=math)
     gy = _r(*y.shape, seed=7).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split", 1: "ig_bf16"}[math]
+    kern = {2: "ig_split_halo", 1: "ig_bf16"}[math]  # split: the halo-reusing kernel at these shapes
     pf = _lib.plan("conv_transpose2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv_transpose2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv_transpose2d_wgrad", xd.detach(), gy, 5, 2, 2, math)

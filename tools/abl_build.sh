@@ -1,18 +1,26 @@
 #!/bin/bash
-# Build ablation variants of libimgcomp.so into tools/_abl/lib_<tag>.so:
+# Build an ablation variant of the library pair into tools/_abl/<tag>/:
 #   bash tools/abl_build.sh TAG "-DMACRO=VAL ..."
-# (the GPU side selects one with IMGCOMP_LIB=tools/_abl/lib_TAG.so)
+# libimgcomp.so with the macros and its own libimgcomp_torch.so (rpath $ORIGIN, so torch.ops.imgcomp
+# calls the variant too).  The GPU side selects it with IMGCOMP_LIB=tools/_abl/TAG/libimgcomp.so
 set -e
 TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/image_compression_amd/csrc
 B=$R/tools/_abl/build_$TAG
-mkdir -p $B
+O=$R/tools/_abl/$TAG
+mkdir -p $B $O
+NOPK_SRCS=${NOPK_SRCS-"entropy elementwise msssim metrics optim"}   # as the Makefile (override: NOPK_SRCS=...)
 for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics; do
-  if [ "$f" = "igemm" ] || [ "$f" = "wgrad" ] || [ "$f" = "gdn_fused" ] || [ "$f" = "edge" ] || [ ! -f $B/$f.o ]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C "$@" -c $C/$f.hip -o $B/$f.o &
-  fi
+  extra=""
+  case " $NOPK_SRCS " in *" $f "*) extra="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C $extra "$@" -c $C/$f.hip -o $B/$f.o 2>&1 \
+    | grep -v "not a recognized feature" &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/tools/_abl/lib_$TAG.so $B/*.o
-echo built tools/_abl/lib_$TAG.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libimgcomp.so $B/*.o
+TORCH_DIR=$(python3 -c 'import os, torch; print(os.path.dirname(torch.__file__))')
+g++ -shared -o $O/libimgcomp_torch.so $C/build/torch_ops.o -L$O -limgcomp -L$TORCH_DIR/lib -ltorch -ltorch_cpu -lc10 \
+  -lc10_hip -ltorch_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$TORCH_DIR/lib
+rm -rf $B
+echo built tools/_abl/$TAG/
