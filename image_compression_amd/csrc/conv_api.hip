@@ -340,7 +340,9 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   d.Hx = X->h; d.Wx = X->w; d.Cx = X->c;
   d.N = G->n; d.stride = stride; d.T = k * k; d.x_op = AOP_NONE;
   d.generic = (X->c % 4 != 0) || (X->sc != 1);
-  d.x3 = (math & IC_MATH_SPLIT) ? 1 : 0;
+  d.split_ok = (math & IC_MATH_SPLIT) ? 1 : 0;
+  d.bf16 = (math & IC_MATH_BF16) ? 1 : 0;
+  d.x3 = (d.split_ok || d.bf16) ? 1 : 0;  // the bf16 form runs on the split kernel family
   int kk_of_t[IC_MAXT];
   for (int t = 0; t < d.T; ++t) {
     d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
@@ -376,6 +378,7 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
     d.xs_c = 1; d.xs_w = Kp; d.xs_h = (long long)G->w * Kp; d.xs_n = (long long)G->h * G->w * Kp;
     d.generic = 0;
     d.x3 = 0;
+    d.bf16 = 0;
   }
   const size_t part = wg_plan(d);
   const size_t cs = db ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;

@@ -105,7 +105,7 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
       wsb >= fused_ws)
     return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s,
-                         (math & IC_MATH_SPLIT) ? 1 : 0, dxsum);
+                         (math & IC_MATH_BF16) && x->c == 192 ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0, dxsum);
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};
@@ -182,7 +182,10 @@ int gdn_plan(int bwd, const ic_act* x, int math) {
       return IC_OK;
     }
   } else if (fused) {
-    plan_report(split && x->c == 192 ? IC_KERNEL_GDN_FUSED_SPLIT : IC_KERNEL_GDN_FUSED, 16, x->c, 1, 0, 0, -1);
+    plan_report((math & IC_MATH_BF16) && x->c == 192 ? IC_KERNEL_GDN_FUSED_BF16
+                : split && x->c == 192                  ? IC_KERNEL_GDN_FUSED_SPLIT
+                                                        : IC_KERNEL_GDN_FUSED,
+                16, x->c, 1, 0, 0, -1);
     return IC_OK;
   }
   size_t n = 0;

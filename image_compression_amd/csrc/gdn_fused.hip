@@ -399,7 +399,8 @@ __global__ void __launch_bounds__(768, 1)
 // X3: also write q and x^2, split into three bf16 terms, as [pixel][channel]
 // images (sb: q planes then x^2 planes, unpadded C-wide rows whose 16-B chunks
 // are XOR-swizzled by 4 on rows with bit 1 set) for the split dgamma GEMM
-template <int C, int BM, bool X3 = false>
+// BF: bf16 operands (config C3): only the first plane, q and x^2 rounded to nearest even
+template <int C, int BM, bool X3 = false, bool BF = false>
 __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
                                                 uint32_t P, int inverse, int tid, __bf16* sb = nullptr) {
   constexpr int NCH = BM * C / 4;
@@ -434,6 +435,13 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
       constexpr int PL = BM * C;  // one plane
 #pragma unroll
       for (int op = 0; op < 2; ++op) {
+        if constexpr (BF) {
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          const floatx4v v = op == 0 ? qv : xv * xv;
+          *(b4*)(sb + op * PL + m * C + col) =
+              __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
+          continue;
+        }
         b4 vh, vm, vl;
         if (GDN_SPLIT_PK) {
           split3_bf16x4(op == 0 ? qv : xv * xv, vh, vm, vl);
@@ -495,12 +503,19 @@ __device__ unsigned long long gdn_prof[256 * 8 * 16 * 6];
 // images, read transposed (ds_read_b64_tr_b16, 8 pixels of one channel per
 // lane); waves 4-7 own 96x96 quadrants of dgamma.  Group A's dx GEMM keeps
 // gamma in VGPRs on the fp32 MFMA.
-template <int C, bool X3>
+//
+// BF (C = 192, with X3; IC_MATH_BF16, config C3): both GEMMs on bf16 operands with fp32
+// accumulation — group A holds gamma as bf16 16x16x32 B fragments (72 VGPRs) and reads q's
+// A fragments from the fp32 q image (8 channels per lane, rounded in registers); group B runs
+// the quadrant GEMM with one product on single bf16 planes of q and x^2.
+template <int C, bool X3, bool BF = false>
 __global__ void __launch_bounds__(512, 2)
     gdn_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
                          const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
                          float* __restrict__ slab, uint32_t P) {
   static_assert(!X3 || C == 192, "split dgamma tiles 192 x 192 as 2 x 2 quadrants of 96");
+  static_assert(!BF || X3, "bf16 operands run on the split kernel's layout");
+  constexpr int NP = BF ? 1 : 3;  // bf16 planes per operand image
   constexpr int BM = 16;
   constexpr int NTA = 256;       // threads of group A (staging / copy-out)
   constexpr int W4 = C / 4;      // channels per wave slice
@@ -511,7 +526,7 @@ __global__ void __launch_bounds__(512, 2)
   constexpr int NSTORE = BM * C / 4 / NTA;
   // per buffer: x, norm, dy images; plus the q image
   __shared__ __attribute__((aligned(16))) float lds[7 * TILE];
-  __shared__ __attribute__((aligned(16))) __bf16 sbf[X3 ? 6 * TILE : 8];  // split q / x^2 images
+  __shared__ __attribute__((aligned(16))) __bf16 sbf[X3 ? 2 * NP * TILE : 8];  // split q / x^2 images
   float* const qs = lds + 6 * TILE;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -533,7 +548,20 @@ __global__ void __launch_bounds__(512, 2)
   if (w < 4) {
     // ---------------- group A: dxg[m][k] = sum_n q[m][n] gamma[n][k], k = wbase + 16j + li
     // step s = 4u+v: n = 16u + 4lq + v  ->  bfr[j][4u+v] = gamma[n][k]
-    float bfr[NTW][4 * KU];
+    // BF: 16x16x32 step s32: n = 32 s32 + 8 lq + e  ->  gbf[j][s32][e] = bf16(gamma[n][k])
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    constexpr int K32 = C / 32;
+    float bfr[BF ? 1 : NTW][BF ? 1 : 4 * KU];
+    b8 gbf[BF ? NTW : 1][BF ? K32 : 1];
+    if constexpr (BF) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int s32 = 0; s32 < K32; ++s32)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            gbf[j][s32][e] = (__bf16)gamma[(size_t)(32 * s32 + 8 * lq + e) * C + wbase + 16 * j + li];
+    } else {
 #pragma unroll
     for (int j = 0; j < NTW; ++j)
 #pragma unroll
@@ -541,6 +569,7 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           bfr[j][4 * u + v] = gamma[(size_t)(16 * u + 4 * lq + v) * C + wbase + 16 * j + li];
+    }
     uint32_t tile = blockIdx.x;
     if (tile < ntiles) stage(tile, 0, tid);
     int buf = 0, it = 0;
@@ -554,13 +583,27 @@ __global__ void __launch_bounds__(512, 2)
       const uint32_t nxt = tile + gridDim.x;
       float* xs = lds + buf * 3 * TILE;
       float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
-      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
+      gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
       GDN_MARK(it, 2);
       floatx4v acc[NTW];
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
+        // A fragment of step s32: q[m = li][32 s32 + 8 lq .. + 7] = logical chunks 8 s32 + 2 lq (+1)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int s32 = 0; s32 < K32; ++s32) {
+          const int c0 = 8 * s32 + 2 * lq;
+          const floatx4v lo = *(const floatx4v*)(qs + li * C + ((c0 ^ li) << 2));
+          const floatx4v hi = *(const floatx4v*)(qs + li * C + (((c0 + 1) ^ li) << 2));
+          const b8 a = __builtin_bit_cast(b8, u32x4{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3]),
+                                                     ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, gbf[j][s32], acc[j], 0, 0, 0);
+        }
+      } else
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         const floatx4v a4 = *(const floatx4v*)(qs + li * C + (((4 * u + lq) ^ li) << 2));
@@ -631,7 +674,7 @@ __global__ void __launch_bounds__(512, 2)
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
       if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
-      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
+      gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
       GDN_MARK(it, 2);
@@ -639,18 +682,22 @@ __global__ void __launch_bounds__(512, 2)
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
       }
-      b8 bb[3][3];
+      b8 bb[NP][3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NP; ++q)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) bb[q][j] = tr8(sbf + 3 * PL + q * PL + tr_row + ((96 * wn2 + 32 * j + tr_col) ^ tr_sw));
+        for (int j = 0; j < 3; ++j) bb[q][j] = tr8(sbf + NP * PL + q * PL + tr_row + ((96 * wn2 + 32 * j + tr_col) ^ tr_sw));
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        b8 a[3];
+        b8 a[NP];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) a[q] = tr8(sbf + q * PL + tr_row + ((96 * wm2 + 32 * i + tr_col) ^ tr_sw));
+        for (int q = 0; q < NP; ++q) a[q] = tr8(sbf + q * PL + tr_row + ((96 * wm2 + 32 * i + tr_col) ^ tr_sw));
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
+          if constexpr (BF) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
+            continue;
+          }
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0][j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1][j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2][j], acc[i][j], 0, 0, 0);
@@ -704,7 +751,7 @@ __global__ void __launch_bounds__(512, 2)
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
       if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
-      gdn_bwd_phase_a<C, BM, X3>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
+      gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
       GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
       GDN_MARK(it, 2);
@@ -835,13 +882,13 @@ int bwd_grid(long long P) {
   return (int)(ntiles < 256 ? ntiles : 256);
 }
 
-template <int C, bool X3 = false>
+template <int C, bool X3 = false, bool BF = false>
 int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
                          float* dx, float* dgamma, float* dbeta, float* dxsum, long long P, float* slab,
                          hipStream_t s) {
   const int grid = bwd_grid(P);
   if (grid < 1) return IC_OK;
-  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx,
+  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3, BF>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx,
                      slab, (uint32_t)P);
   IC_CHECK_LAUNCH();
   const int stride = GDN_SLAB(C);
@@ -887,6 +934,8 @@ size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * GDN_S
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {
   float* slab = (float*)ws;
+  if (split == 2 && C == 192)
+    return gdn_bwd_fused_launch<192, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   if (split && C == 192)
     return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   switch (C) {

@@ -32,10 +32,6 @@ struct IgPhase {
   long long m_off;  // row offset of this phase inside the split-K partial buffer
   FastDiv fd_hw, fd_w;  // divide by Hg*Wg and by Wg
   int dy[IC_MAXT], dx[IC_MAXT];
-  // halo tiles (ig_kernel_halo, set by ig_plan): a tile is hrows whole rows of the output grid;
-  // its input patch spans rows gy0*stride + hdy0 + [0, hph) and columns hdx0 + [0, hpw), stored
-  // with hpw_l pixels per row (stride 2: even columns, then odd ones from hpw2)
-  int hrows, hdy0, hdx0, hph, hpw, hpw2, hpw_l;
 };
 
 struct IgDesc {
@@ -62,7 +58,6 @@ struct IgDesc {
   int x3;            // fp32 by exact three-term bf16 split (fast path, Cin % 32 == 0); wp holds three
                      // bf16 planes [part][t][Npad][Cin], part p at wp + p * wplane (bf16 elements)
   long long wplane;
-  int halo;          // split tiles on ig_kernel_halo (set by ig_plan)
   IgPhase ph[IC_MAXPH];
 };
 
@@ -95,6 +90,9 @@ struct WgDesc {
   int rowfast;     // Wg and pixels-per-split multiples of the 16-pixel K step (set by wg_run)
   float* partial;  // [nsplit][Tp][Cg][ncols]
   int x3;          // fp32 by exact three-term bf16 split (wg_x3_kernel); cleared by wg_plan when unsupported
+  int bf16;        // with x3: bf16 operands on the two-wave kernel (wg_x3d_kernel<..., 1>); cleared by wg_plan
+                   // where that kernel does not run
+  int split_ok;    // split arithmetic allowed (IC_MATH_SPLIT): wg_plan's fallback when bf16 is cleared
   int dy[IC_MAXT], dx[IC_MAXT];
 };
 
@@ -159,7 +157,8 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0,
-                  float* dxsum = nullptr);  // dxsum: column sums of dx over all pixels (C), when non-null
+                  float* dxsum = nullptr);  // split: 1 split dgamma, 2 bf16 operands in both GEMMs (C = 192);
+                                            // dxsum: column sums of dx over all pixels (C), when non-null
 
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,

@@ -739,396 +739,6 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
 }
 
-// ------------------------------------------------------------------ split, A in registers
-// The split implicit GEMM with no LDS image of A: each wave gathers its own
-// 64 rows x 32 channels of the K chunk straight from global memory in the
-// 16x16x32 A-fragment layout (lane (r, g): row r, channels 8g .. 8g+7, two
-// 16-B loads per 16-row tile) and splits them in registers; the two waves of
-// a block that share those rows read the same lines, the second from L1.
-// Only B — the three pre-split weight planes, 36 KB per chunk at BN = 192 —
-// goes through LDS, by LDS-DMA (global_load_lds_dwordx4 from inline asm: no
-// VGPR staging, no ds_write), into two stages (72 KB, two blocks per CU),
-// with ONE barrier per chunk: at the top of chunk c every wave waits for its
-// own DMA of B(c) and its loads of A(c) (vmcnt(0)) and the barrier publishes
-// B(c) and retires every read of the stage that B(c+1) then overwrites.
-// Per chunk: barrier, split A(c) (32 values per lane), issue DMA B(c+1) and
-// the loads of A(c+1), then the 144 MFMAs of chunk c.  The MFMAs are the
-// same six products in the same order as ig_kernel_x3s, so the result is
-// bitwise that kernel's.  The DMA source addresses carry the B swizzle
-// (ig_swz): lane L of a DMA instruction lands in LDS slot L & 3 of row L >> 2
-// and fetches the logical 16-B chunk (L & 3) ^ ig_swz(row) of its row.
-#ifndef IG_X3R
-#define IG_X3R 0  // 1: 128-row split tiles on ig_kernel_x3r (measured 4 % slower than ig_kernel_x3s, r03b)
-#endif
-
-__device__ __attribute__((aligned(16))) float ig_zero_page8[8];
-
-// 16 B per lane, global -> LDS at byte offset lds + 16 * lane (wave-uniform lds)
-__device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
-  uint32_t save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(save)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
-
-#ifndef IG_X3R_SGB
-#define IG_X3R_SGB 2  // ig_kernel_x3r: one A load per IG_X3R_SGB MFMAs at the top of the chunk's MFMAs
-#endif
-
-template <int BM, int BN, int WM, int WN, bool SQ>
-__global__ void __launch_bounds__(256, 2) ig_kernel_x3r(const IgDesc d) {
-  constexpr int NP = 3, LDB = 32;
-  constexpr int WAVES_N = BN / WN;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int BROWS = NP * BN;           // 64-B rows per B stage
-  constexpr int BSTAGE = BROWS * LDB;      // bf16 elements per stage
-  constexpr int NDMA = BROWS / 16 / 4;     // 1-KB DMA instructions per wave per chunk
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(BROWS % 64 == 0, "whole DMA instructions per wave");
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2 * BSTAGE];
-
-  const int zi = blockIdx.z;
-  const int phase = zi / d.ksplit;
-  const int split = zi - phase * d.ksplit;
-  const IgPhase& P = d.ph[phase];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  const int n0 = blockIdx.y * BN;
-  const int T = P.T;
-  const int nchunks = T * (d.Cin >> 5);
-  const int cb = split * d.kcps;
-  const int ce = min(nchunks, cb + d.kcps);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w / WAVES_N, wn = w - (w / WAVES_N) * WAVES_N;
-  const int r = lane & 15, g = lane >> 4;
-  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
-
-  // A: this lane's rows m0 + wm*WM + 16 i + r
-  uint32_t a_off[TM];
-  int a_iy[TM], a_ix[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const uint32_t m = m0 + wm * WM + 16 * i + r;
-    const bool ok = m < M;
-    const uint32_t mm = ok ? m : 0u;
-    const uint32_t img = fdiv(mm, P.fd_hw);
-    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
-    const uint32_t gy = fdiv(rem, P.fd_w);
-    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
-    a_iy[i] = ok ? (int)gy * d.stride : -0x40000000;  // invalid rows fail the bounds test
-    a_ix[i] = (int)gx * d.stride;
-    a_off[i] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[i] * xsh + (uint32_t)a_ix[i] * xsw + 8u * g;
-  }
-  const float* __restrict__ xg = d.x;
-
-  // B: DMA instruction j of this wave moves 64-B rows R = (w*NDMA + j)*16 + (lane >> 2)
-  // (plane R / BN, row R % BN), slot lane & 3 <- logical chunk (lane & 3) ^ ig_swz(row)
-  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-  uint32_t b_src[NDMA];
-#pragma unroll
-  for (int j = 0; j < NDMA; ++j) {
-    const int R = (w * NDMA + j) * 16 + (lane >> 2);
-    const int q = R / BN, row = R - (R / BN) * BN;
-    b_src[j] = (uint32_t)(q * d.wplane) + (uint32_t)(n0 + row) * (uint32_t)d.Cin + 8u * ((lane & 3) ^ ig_swz(row));
-  }
-  // LDS byte offset of this wave's DMA rows in stage 0
-  const uint32_t lds_b = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) __bf16*)Bs + (uint32_t)(w * NDMA * 16 * LDB * 2));
-  const size_t tstride = (size_t)d.Npad * d.Cin;
-  auto dma_b = [&](int cc, int t, int stage) {
-    const __bf16* base = wpb + (size_t)t * tstride + cc * 32;
-    const uint32_t dst = lds_b + (uint32_t)(stage * BSTAGE * 2);
-#pragma unroll
-    for (int j = 0; j < NDMA; ++j) ig_glds16(base + b_src[j], dst + (uint32_t)(j * 16 * LDB * 2));
-  };
-
-  floatx4v raw[TM][2];
-  auto load_a = [&](int cc, int t) {
-    const int dy = P.dy[t], dx = P.dx[t];
-    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
-      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
-      const float* src = in ? xg + (a_off[i] + toff) : ig_zero_page8;
-      raw[i][0] = *(const floatx4v*)src;
-      raw[i][1] = *(const floatx4v*)(src + 4);
-    }
-  };
-
-  floatx4v acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-
-  // chunk c = (channel chunk cc, tap t): channel chunk outer, tap inner (as ig_kernel_x3s)
-  int cc = cb / T, t = cb - (cb / T) * T;
-  if (cb < ce) {
-    dma_b(cc, t, 0);
-    load_a(cc, t);
-  }
-  const int ch = 8 * (g ^ ig_swz(r));
-  for (int c = cb; c < ce; ++c) {
-    const int stage = (c - cb) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // split A(c): a[q][i] = plane q (hi, mid, lo) of rows 16 i + r, channels 8g .. 8g+7
-    bf16x8 a[NP][TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      bf16x4 h0, md0, l0, h1, md1, l1;
-      split3_bf16x4(SQ ? raw[i][0] * raw[i][0] : raw[i][0], h0, md0, l0);
-      split3_bf16x4(SQ ? raw[i][1] * raw[i][1] : raw[i][1], h1, md1, l1);
-      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[1][i] = __builtin_shufflevector(md0, md1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    const bool more = c + 1 < ce;
-    const int cn = (t + 1 == T) ? cc + 1 : cc, tn = (t + 1 == T) ? 0 : t + 1;
-    if (more) dma_b(cn, tn, stage ^ 1);
-    // unconditional: the last chunk reloads itself (unused), so the loads share the MFMAs' block
-    load_a(more ? cn : cc, more ? tn : t);
-    const __bf16* Brd = Bs + stage * BSTAGE + (wn * WN + r) * LDB + ch;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bf16x8 b[NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
-      }
-    }
-    if constexpr (IG_X3R_SGB > 0) {
-      // the next chunk's A loads at the top of this chunk's MFMAs (the compiler would sink them
-      // to the loop end, where the barrier's vmcnt(0) then waits out their whole latency)
-#pragma unroll
-      for (int k = 0; k < 2 * TM; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);            // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x008, IG_X3R_SGB, 0);   // MFMA
-      }
-    }
-    cc = cn;
-    t = tn;
-  }
-  ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
-}
-
-// ------------------------------------------------------------------ split, halo-reusing A
-// The split implicit GEMM for 128-row tiles of whole output rows, one 8-wave block per CU.
-// K is walked as (16-channel chunk cc) outer, (tap pair) inner: a K-step of 32 is two taps x 16
-// channels.  Instead of gathering the 128 x 32 A slab of every tap from global memory (25 x per
-// channel chunk), the block stages the tile's input PATCH of the chunk once — fp32, rows
-// gy0*s + [hdy0, hdy0 + hph) x columns [hdx0, hdx0 + hpw) x 16 channels, 80-B pixel pitch (16
-// consecutive pixels hit 16 distinct 16-B bank slots), stride-2 gathers with the columns
-// de-interleaved by parity so that a tap's pixels are consecutive — and every tap reads its A
-// fragments from it: lane (r, g) of the 16x16x32 A operand reads the 8 channels (g & 1) of tap
-// (g >> 1) of its pixel (two ds_read_b128) and splits them in registers.  B — the three
-// pre-split weight planes of the two taps, 36 KB — arrives by LDS-DMA into two stages (one barrier
-// per K-step); its 64-B rows hold [tap a: 16 ch | tap b: 16 ch], the layout ig_kernel_x3s uses for
-// one tap x 32 channels, with the same chunk swizzle.  The next chunk's patch is loaded into
-// registers during the chunk's last K-step and written to LDS behind one extra barrier.  An odd
-// tap count pads the last pair with zero weights (4 % of the MFMAs at 25 taps).  Eight waves of
-// 32 x 96; the MFMA sequence per (i, j) and K-step is ig_kernel_x3s's six products.
-#ifndef IG_HALO
-#define IG_HALO 1
-#endif
-constexpr int HALO_PITCH = 20;         // floats per patch pixel: 16 channels + 4 pad
-constexpr int HALO_PATCH_MAX = 18560;  // floats of the patch image (72.5 KB; 7 x 132 pixels at g_a.2)
-constexpr int HALO_KP = 8;             // 16-B patch pieces per thread (512 threads): patches <= 1024 pixels
-
-__device__ __attribute__((aligned(16))) float ig_zero16[4];
-
-template <bool SQ>
-__global__ void __launch_bounds__(512, 1) ig_kernel_halo(const IgDesc d) {
-  constexpr int BM = 128, BN = 192, NP = 3, LDB = 32;
-  constexpr int WM = 32, WN = 96, TM = WM / 16, TN = WN / 16;
-  constexpr int BROWS = NP * BN;          // 64-B rows per B stage
-  constexpr int BSTAGE = BROWS * LDB;     // bf16 elements per stage (36 KB)
-  constexpr int NDMA_ALL = BROWS / 16;    // 1-KB DMA instructions per stage (36)
-  constexpr int NDMA = (NDMA_ALL + 7) / 8;
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2 * BSTAGE];
-  __shared__ __attribute__((aligned(16))) float Ps[HALO_PATCH_MAX];
-
-  const IgPhase& P = d.ph[blockIdx.z];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (DMA bases go to M0)
-  const int wm = w >> 1, wn = w & 1;
-  const int r = lane & 15, g = lane >> 4;
-  const int s = d.stride;
-  const int T = P.T, NPAIR = (T + 1) >> 1, CC = d.Cin >> 4;
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  // tile = hrows whole rows gy0 .. of image img (ig_plan: tiles never cross an image)
-  const uint32_t img = fdiv(m0, P.fd_hw);
-  const int gy0 = (int)fdiv(m0 - img * P.fd_hw.d, P.fd_w);
-  const int iy0 = gy0 * s + P.hdy0, ix0 = P.hdx0;
-  const float* __restrict__ xg = d.x + (size_t)img * (size_t)d.xs_n;
-
-  // ---- patch pieces of this thread: pixel e >> 2, channel quad e & 3 (fixed for the tile)
-  const int npix = P.hph * P.hpw;
-  uint32_t pg[HALO_KP];   // element offset from xg (0xffffffff: zero padding)
-  uint32_t pl[HALO_KP];   // float offset in Ps (0xffffffff: no piece)
-#pragma unroll
-  for (int k = 0; k < HALO_KP; ++k) {
-    const int e = tid + 512 * k;
-    const int pix = e >> 2, q4 = e & 3;
-    pg[k] = 0xffffffffu;
-    pl[k] = 0xffffffffu;
-    if (pix < npix) {
-      const int prow = pix / P.hpw, pcol = pix - (pix / P.hpw) * P.hpw;
-      const int iy = iy0 + prow, ix = ix0 + pcol;
-      const int pc = s == 2 ? (pcol & 1) * P.hpw2 + (pcol >> 1) : pcol;
-      pl[k] = (uint32_t)((prow * P.hpw_l + pc) * HALO_PITCH + 4 * q4);
-      if ((unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx)
-        pg[k] = (uint32_t)iy * (uint32_t)d.xs_h + (uint32_t)ix * (uint32_t)d.xs_w + 4u * q4;
-    }
-  }
-  floatx4v pre[HALO_KP];
-  auto patch_load = [&](int cc) {
-#pragma unroll
-    for (int k = 0; k < HALO_KP; ++k) {
-      const float* src = pg[k] != 0xffffffffu ? xg + pg[k] + 16 * cc : ig_zero16;
-      pre[k] = *(const floatx4v*)src;
-    }
-  };
-  auto patch_store = [&]() {
-#pragma unroll
-    for (int k = 0; k < HALO_KP; ++k)
-      if (pl[k] != 0xffffffffu) *(floatx4v*)&Ps[pl[k]] = SQ ? pre[k] * pre[k] : pre[k];
-  };
-
-  // ---- A: this lane's pixels m = wm*32 + 16 i + r of the tile: patch offset of tap (hdy0, hdx0)
-  int a_base[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wm * WM + 16 * i + r;
-    const int ry = m / P.Wg, gx = m - (m / P.Wg) * P.Wg;
-    a_base[i] = (ry * s * P.hpw_l + gx) * HALO_PITCH + 8 * (g & 1);
-  }
-  // patch offset of tap t relative to a_base (stride 2: parity plane + half column)
-  auto tapoff = [&](int t) {
-    const int dyr = P.dy[t] - P.hdy0, dxr = P.dx[t] - P.hdx0;
-    const int c = s == 2 ? (dxr & 1) * P.hpw2 + (dxr >> 1) : dxr;
-    return (dyr * P.hpw_l + c) * HALO_PITCH;
-  };
-
-  // ---- B: DMA instruction q = w + 8 j moves 64-B rows R = 16 q + (lane >> 2) (plane R / BN,
-  // row R % BN); slot lane & 3 <- logical chunk (lane & 3) ^ ig_swz(row) = (tap lc >> 1, half lc & 1)
-  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-  uint32_t b_off[NDMA];
-  bool b_tapb[NDMA];
-#pragma unroll
-  for (int j = 0; j < NDMA; ++j) {
-    const int q = w + 8 * j;
-    const int R = 16 * q + (lane >> 2);
-    const int pl_ = R / BN, row = R - (R / BN) * BN;
-    const int lc = (lane & 3) ^ ig_swz(row);
-    b_off[j] = (uint32_t)(pl_ * d.wplane) + (uint32_t)row * (uint32_t)d.Cin + 8u * (lc & 1);
-    b_tapb[j] = (lc >> 1) != 0;
-  }
-  const uint32_t lds_b = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) __bf16*)Bs);
-  const size_t tstride = (size_t)d.Npad * d.Cin;
-  auto dma_b = [&](int cc, int p, int buf) {
-    const int ta = 2 * p, tb = 2 * p + 1;
-    const __bf16* base_a = wpb + (size_t)ta * tstride + 16 * cc;
-    const __bf16* base_b = tb < T ? wpb + (size_t)tb * tstride + 16 * cc : nullptr;
-    const uint32_t dst = lds_b + (uint32_t)(buf * BSTAGE * 2);
-#pragma unroll
-    for (int j = 0; j < NDMA; ++j) {
-      const int q = w + 8 * j;
-      if (q < NDMA_ALL) {
-        const void* src = b_tapb[j] ? (base_b ? (const void*)(base_b + b_off[j]) : (const void*)ig_zero16)
-                                    : (const void*)(base_a + b_off[j]);
-        ig_glds16(src, dst + (uint32_t)(q * 16 * LDB * 2));
-      }
-    }
-  };
-
-  floatx4v acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: patch of chunk 0, B of K-step 0
-  patch_load(0);
-  dma_b(0, 0, 0);
-  patch_store();
-  const int ch = 8 * (g ^ ig_swz(r));
-  const int nsteps = CC * NPAIR;
-  int cc = 0, p = 0;
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // B(st) and the patch of cc published; every read of buffer buf ^ 1 retired
-    const bool last_pair = p == NPAIR - 1;
-    const int cn = last_pair ? cc + 1 : cc, pn = last_pair ? 0 : p + 1;
-    if (st + 1 < nsteps) dma_b(cn, pn, buf ^ 1);
-    if (last_pair && cc + 1 < CC) patch_load(cc + 1);
-    // A fragments of the pair: lanes g >> 1 = 0 tap 2p, = 1 tap 2p + 1 (odd T: reuse tap 2p, B is 0)
-    const int ta = 2 * p, tb = 2 * p + 1 < T ? 2 * p + 1 : 2 * p;
-    const int toff = (g >> 1) ? tapoff(tb) : tapoff(ta);
-    bf16x8 a[NP][TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* src = Ps + a_base[i] + toff;
-      const floatx4v v0 = *(const floatx4v*)src, v1 = *(const floatx4v*)(src + 4);
-      bf16x4 h0, md0, l0, h1, md1, l1;
-      split3_bf16x4(v0, h0, md0, l0);
-      split3_bf16x4(v1, h1, md1, l1);
-      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[1][i] = __builtin_shufflevector(md0, md1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    const __bf16* Brd = Bs + buf * BSTAGE + (wn * WN + r) * LDB + ch;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bf16x8 b[NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) b[q] = *(const bf16x8*)(Brd + (q * BN + j * 16) * LDB);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
-      }
-    }
-    if (last_pair && cc + 1 < CC) {
-      // every wave is done with this chunk's patch (its fragment reads fed the MFMAs above)
-      __syncthreads();
-      patch_store();  // published by the next K-step's barrier
-    }
-    cc = cn;
-    p = pn;
-  }
-  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, 0);
-}
-
 // split-K reduction + epilogue: one thread per (row, channel)
 __global__ void ig_reduce_kernel(const IgDesc d) {
   const long long total = d.Mtot * d.Cout;
@@ -1181,14 +791,10 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
       return IC_ERR_ARG;
     case IC_KERNEL_IG_SPLIT:
       if constexpr (BN % 64 == 0 && BM == 128) {
-        if (IG_X3R) {
-          if (sq) hipLaunchKernelGGL((ig_kernel_x3r<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
-          else hipLaunchKernelGGL((ig_kernel_x3r<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
-          break;
-        }
+
       }
       if constexpr (BN % 64 == 0) {
-        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN>), grid, dim3(256), 0, s, d);
+        hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN>), grid, dim3(64 * (BM / WM) * (BN / WN)), 0, s, d);
         break;
       }
       return IC_ERR_ARG;
@@ -1220,35 +826,7 @@ int ig_npad(int Cout) {
 #define IG_KSPLIT_MAX 32  // more splits cost more in the partial-sum pass than they save
 #endif
 
-// ig_kernel_halo takes split 128 x 192 tiles of whole output rows whose input patch fits its LDS image
-static void ig_plan_halo(IgDesc& d, long long tiles) {
-  d.halo = 0;
-  if (!IG_HALO || !d.x3 || d.bf16 || d.generic || d.bm != 128 || d.bn != 192 || d.Npad != 192) return;
-  if (d.Cin % 16 != 0 || d.xs_c != 1 || d.a_op == AOP_ABS || (d.stride != 1 && d.stride != 2)) return;
-  if (tiles < 256) return;  // one block per CU
-  for (int p = 0; p < d.nphase; ++p) {
-    IgPhase& P = d.ph[p];
-    if (P.Wg < 1 || P.Wg > 128 || 128 % P.Wg != 0) return;
-    P.hrows = 128 / P.Wg;
-    if (P.Hg % P.hrows != 0) return;
-    int dy0 = P.dy[0], dy1 = P.dy[0], dx0 = P.dx[0], dx1 = P.dx[0];
-    for (int t = 1; t < P.T; ++t) {
-      dy0 = P.dy[t] < dy0 ? P.dy[t] : dy0; dy1 = P.dy[t] > dy1 ? P.dy[t] : dy1;
-      dx0 = P.dx[t] < dx0 ? P.dx[t] : dx0; dx1 = P.dx[t] > dx1 ? P.dx[t] : dx1;
-    }
-    P.hdy0 = dy0;
-    P.hdx0 = dx0;
-    P.hph = (P.hrows - 1) * d.stride + (dy1 - dy0) + 1;
-    P.hpw = (P.Wg - 1) * d.stride + (dx1 - dx0) + 1;
-    P.hpw2 = (P.hpw + 1) / 2;
-    P.hpw_l = d.stride == 2 ? 2 * P.hpw2 : P.hpw;
-    if (P.hph * P.hpw > HALO_KP * 512 / 4 || P.hph * P.hpw_l * HALO_PITCH > HALO_PATCH_MAX) return;
-  }
-  d.halo = 1;
-}
-
 size_t ig_plan(IgDesc& d) {
-  d.halo = 0;
   long long mall = 0;
   for (int p = 0; p < d.nphase; ++p) mall += (long long)d.N * d.ph[p].Hg * d.ph[p].Wg;
   if (d.Cout % 192 == 0) {
@@ -1292,7 +870,6 @@ size_t ig_plan(IgDesc& d) {
   if (d.ksplit <= 1) {
     d.ksplit = 1;
     d.kcps = nchunks_max;
-    ig_plan_halo(d, tiles);
     return 0;
   }
   return (size_t)d.ksplit * (size_t)mtot * (size_t)d.Cout * sizeof(float);
@@ -1300,7 +877,7 @@ size_t ig_plan(IgDesc& d) {
 
 int ig_kernel_kind(const IgDesc& d) {
   if (d.bf16) return ig_bf16_wide(d) ? IC_KERNEL_IG_BF16 : IC_KERNEL_IG_SPLIT_BF16;
-  if (d.x3) return d.halo ? IC_KERNEL_IG_SPLIT_HALO : IC_KERNEL_IG_SPLIT;
+  if (d.x3) return IC_KERNEL_IG_SPLIT;
   return d.generic ? IC_KERNEL_IG_FP32_GATHER : IC_KERNEL_IG_FP32;
 }
 
@@ -1317,15 +894,6 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
-  if (d.halo) {
-    int mt = 0;
-    for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
-    const dim3 grid(mt, 1, d.nphase);
-    if (d.a_op == AOP_SQUARE) hipLaunchKernelGGL(ig_kernel_halo<true>, grid, dim3(512), 0, s, d);
-    else hipLaunchKernelGGL(ig_kernel_halo<false>, grid, dim3(512), 0, s, d);
-    IC_CHECK_LAUNCH();
-    return IC_OK;
-  }
   if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
   else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);

@@ -726,8 +726,10 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
 #endif
 // SEG16: maps 16 wide — a 32-pixel step spans two output rows, each 16-pixel half
-// with its own row base (either half stays inside one row when Wg % 16 == 0)
-template <bool XSQ, bool SEG16>
+// with its own row base (either half stays inside one row when Wg % 16 == 0).
+// NP = 1: bf16 operands (round to nearest even) with fp32 accumulation, one product per
+// tile and step (IC_MATH_BF16, config C3); only plane 0 of each operand image is used.
+template <bool XSQ, bool SEG16, int NP = 3>
 __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
@@ -819,9 +821,15 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
     __bf16* base = lds + buf * STAGE;
 #pragma unroll
     for (int op = 0; op < 2; ++op) {
-      b4 vh, vm, vl;
-      split3_bf16x4(op == 0 ? rg[q] : rx[q], vh, vm, vl);
       __bf16* dst = base + op * OPER + srow[q] * PITCH + (scol[q] ^ swz(srow[q]));
+      const floatx4v v = op == 0 ? rg[q] : rx[q];
+      if constexpr (NP == 1) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        *(b4*)dst = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
+        continue;
+      }
+      b4 vh, vm, vl;
+      split3_bf16x4(v, vh, vm, vl);
       *(b4*)dst = vh;
       *(b4*)(dst + PLANE) = vm;
       *(b4*)(dst + 2 * PLANE) = vl;
@@ -854,21 +862,25 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
       const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * PITCH));
       return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
-    b8 bb[3][TN];
+    b8 bb[NP][TN];
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < NP; ++q)
 #pragma unroll
       for (int j = 0; j < TN; ++j) bb[q][j] = tr8(sb + OPER + q * PLANE, wn * WN + 16 * j);
     const int pn = p0 + 3 * BK;
     const StepBase nb = step_base(pn, pn < pe);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      b8 a[3];
+      b8 a[NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[q] = tr8(sb + q * PLANE, wm * WM + 16 * i);
+      for (int q = 0; q < NP; ++q) a[q] = tr8(sb + q * PLANE, wm * WM + 16 * i);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         floatx4v& c = acc[i][j];
+        if constexpr (NP == 1) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
+          continue;
+        }
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bb[0][j], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[1][j], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[2][j], c, 0, 0, 0);
@@ -880,6 +892,7 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
         // the next step's split + store of slot i / 2, then its refill three steps ahead
         sstore_q(buf ^ 1, i >> 1, rg, rx);
         gload_q(nb, i >> 1, rg, rx);
+        if constexpr (NP == 3)
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);   // MFMA (this and the previous row tile)
@@ -1016,12 +1029,20 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
   if (WG_X3_DUAL && d.rowfast && d.Wg % 32 == 0 && d.pps % 32 == 0) {
-    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false>), grid, dim3(512), 0, s, d);
+    if (d.bf16) {
+      if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false, 1>), grid, dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((wg_x3d_kernel<false, false, 1>), grid, dim3(512), 0, s, d);
+    } else if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false>), grid, dim3(512), 0, s, d);
     else hipLaunchKernelGGL((wg_x3d_kernel<false, false>), grid, dim3(512), 0, s, d);
   } else if (WG_X3_DUAL16 && d.rowfast && d.Wg % 16 == 0 && d.pps % 32 == 0 && d.P % 32 == 0) {
     // whole 32-pixel steps only: with P % 32 == 16 the last split would end on half a step
-    if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, true>), grid, dim3(512), 0, s, d);
+    if (d.bf16) {
+      if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, true, 1>), grid, dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((wg_x3d_kernel<false, true, 1>), grid, dim3(512), 0, s, d);
+    } else if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, true>), grid, dim3(512), 0, s, d);
     else hipLaunchKernelGGL((wg_x3d_kernel<false, true>), grid, dim3(512), 0, s, d);
+  } else if (d.bf16) {
+    return IC_ERR_ARG;  // wg_plan keeps bf16 only where the two-wave kernel runs
   } else if (d.rowfast) {
     if (sq) hipLaunchKernelGGL((wg_x3_kernel<true, true, TWO>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((wg_x3_kernel<true, false, TWO>), grid, dim3(256), 0, s, d);
@@ -1164,6 +1185,13 @@ size_t wg_plan(WgDesc& d) {
   d.pps = (int)pps;
   d.nsplit = (int)((d.P + pps - 1) / pps);
   if (d.nsplit < 1) d.nsplit = 1;
+  // bf16 operands run on the two-wave kernel only (wg_x3_launch's row-fast conditions; pps is a
+  // multiple of 32); elsewhere the split kernel when split arithmetic was asked for, else fp32
+  if (d.bf16 && !(d.x3 && WG_X3_DUAL && WG_X3_DUAL16 && d.Wg % 16 == 0 && (d.Wg % 32 == 0 || d.P % 32 == 0) &&
+                  (long long)d.gs_w * 16 < (1LL << 31) && (long long)d.stride * 16 * d.xs_w < (1LL << 31))) {
+    d.bf16 = 0;
+    if (!d.split_ok) d.x3 = 0;
+  }
   const int Tp = d.generic ? 1 : d.T;
   const size_t slab = (size_t)d.nsplit * Tp * (size_t)d.Cg * d.ncols * sizeof(float);
   const int G = (d.nsplit + WG_SPG - 1) / WG_SPG;
@@ -1185,7 +1213,7 @@ int wg_kernel_kind(const WgDesc& d) {
   const bool glds_ok = d.g_vec && !d.generic && a16(d.g) && a16(d.x) && d.gs_w % 4 == 0 && d.gs_h % 4 == 0 &&
                        d.gs_n % 4 == 0 && d.xs_w % 4 == 0 && d.xs_h % 4 == 0 && d.xs_n % 4 == 0;
   if (d.generic) return IC_KERNEL_WG_FP32_GATHER;
-  if (d.x3) return IC_KERNEL_WG_SPLIT;
+  if (d.x3) return d.bf16 ? IC_KERNEL_WG_BF16 : IC_KERNEL_WG_SPLIT;
   return glds_ok ? IC_KERNEL_WG_LDSDMA : IC_KERNEL_WG_FP32;
 }
 
@@ -1198,6 +1226,7 @@ int wg_run(WgDesc& d, hipStream_t s) {
     case IC_KERNEL_WG_FP32_GATHER:
       return wg_launch_t<192, 64, 96, 32, true>(d, s);
     case IC_KERNEL_WG_SPLIT:
+    case IC_KERNEL_WG_BF16:
       if (!d.g_vec || d.bn != 192 || d.bm != 192) return IC_ERR_ARG;
       return wg_x3_launch(d, s);
     case IC_KERNEL_WG_LDSDMA:

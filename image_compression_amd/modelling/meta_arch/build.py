@@ -21,11 +21,12 @@ def set_compute_dtype(model, dtype):
     terms, six cross products accumulated in fp32, error of an fp32 fma chain
     (functional.MATH) — for the forward, input gradient and weight gradient of
     every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16 operands with fp32
-    accumulation (reduced precision, BASELINE config C3) for the forward and
-    input gradient of the main transforms (g_a, g_s) only — 97 % of the
-    model's FLOPs; the hyperprior transforms (1.3 % of the FLOPs, but they
-    shape the rate term's gradients) and all weight gradients run in
-    "fp32_split" arithmetic there.  GDN,
+    accumulation (reduced precision, BASELINE config C3) for the forward, input
+    gradient and weight gradient of the main transforms (g_a, g_s) — 97 % of the
+    model's FLOPs; where a bf16 kernel does not apply (weight gradients of maps
+    narrower than 16) they fall back to "fp32_split", and the hyperprior
+    transforms (1.3 % of the FLOPs, but they shape the rate term's gradients)
+    run in "fp32_split" arithmetic there.  GDN,
     the entropy models and the 3-channel image edges compute in fp32 in every
     mode, except that "fp32_split" and "bf16" run GDN (C = 192) in split
     arithmetic too: the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at
@@ -38,15 +39,17 @@ def set_compute_dtype(model, dtype):
         raise ValueError(f"compute dtype {dtype!r}: expected one of {sorted(MATH)}")
     main = ("analysis_transform", "synthesis_transform")
     hyper = ("prior_analysis", "prior_synthesis")
-    # IC_MATH_* per transform: bf16 (C3) also runs every weight gradient and the
-    # hyperprior in split arithmetic (fp32-accurate, faster than the fp32 MFMA)
+    # IC_MATH_* per transform: bf16 (C3) falls back to split arithmetic (fp32-accurate,
+    # faster than the fp32 MFMA) where no bf16 kernel applies, and runs the hyperprior split
     split = MATH["fp32_split"]
     flags = {"fp32": (0, 0), "fp32_split": (split, split), "bf16": (MATH["bf16"] | split, split)}[dtype]
     for m in model.modules():
         if isinstance(m, (Conv2d, ConvTranspose2d, GDN)):
             m.math = 0
         if isinstance(m, GDN) and dtype != "fp32":
-            m.math = split      # the fused backward's dgamma GEMM in split arithmetic
+            # the fused backward's dgamma GEMM in split arithmetic; bf16: both of its GEMMs on
+            # bf16 operands (C = 192)
+            m.math = split | (MATH["bf16"] if dtype == "bf16" else 0)
             m.math_fwd = split  # the fused forward (C = 192) in split arithmetic
     for names, flag in ((main, flags[0]), (hyper, flags[1])):
         for name in names:

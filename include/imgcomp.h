@@ -110,8 +110,10 @@ int ic_conv_transpose2d_dgrad_ex(const ic_act* dy, const float* w, int k, int st
                                  const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
 
 /* weight gradients with a math mode: IC_MATH_SPLIT runs the split kernel on 192-channel-tile NHWC
- * operands (>= 128 channels each side), the fp32 kernel otherwise; IC_MATH_BF16 is ignored here
- * (weight gradients stay fp32 in config C3). */
+ * operands (>= 128 channels each side), the fp32 kernel otherwise; IC_MATH_BF16 runs bf16 operands with
+ * fp32 accumulation on the same operands where the two-wave kernel applies (output maps >= 16 wide,
+ * row-aligned 32-pixel steps) and falls back to split arithmetic (when IC_MATH_SPLIT is also set) or
+ * fp32 elsewhere. */
 size_t ic_conv2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, int math);
 int ic_conv2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw, float* db,
                        int math, void* ws, size_t ws_bytes, void* stream);
@@ -135,7 +137,9 @@ size_t ic_gdn_fwd_ws_ex(const ic_act* x, int math);
 int ic_gdn_fwd_ex(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
                   int math, void* ws, size_t ws_bytes, void* stream);
 /* math = IC_MATH_SPLIT: the fused backward (C = 192) forms dgamma in split arithmetic (fp32 via three bf16
- * terms on the bf16 MFMA), dx on the fp32 MFMA.  Other shapes stay on the fp32 MFMA. */
+ * terms on the bf16 MFMA), dx on the fp32 MFMA.  math = IC_MATH_BF16 (C = 192, config C3): both of its
+ * GEMMs (dx's q.gamma and dgamma's q^T x^2) on bf16 operands with fp32 accumulation.  Other shapes stay
+ * on the fp32 MFMA. */
 int ic_gdn_bwd_ex(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                   const ic_act* dx, float* dgamma, float* dbeta, int math, void* ws, size_t ws_bytes, void* stream);
 /* ic_gdn_bwd_ex plus dxsum[c] = sum over all pixels of dx[.,c,.,.] (C floats): the bias gradient of
@@ -184,8 +188,9 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
 #define IC_KERNEL_GDN_FUSED 16      /* gdn_fwd_fused_kernel / gdn_bwd_fused_kernel (fp32 dx) */
 #define IC_KERNEL_GDN_FUSED_SPLIT 17 /* gdn_fwd_x3s_kernel / gdn_bwd_fused_kernel with split dgamma */
 #define IC_KERNEL_GDN_GEMM 18       /* GDN on the implicit GEMM (+ wgrad kernel for dgamma) */
-#define IC_KERNEL_IG_SPLIT_HALO 19  /* ig_kernel_halo: split arithmetic, 128-row tiles, input patch staged once
-                                       per 16-channel chunk and shared by every tap */
+/* 19: retired (a halo-reusing split kernel, measured slower) */
+#define IC_KERNEL_WG_BF16 20        /* wg_x3d_kernel with bf16 operands (one product), fp32 accumulation */
+#define IC_KERNEL_GDN_FUSED_BF16 21 /* gdn_bwd_fused_kernel with bf16 operands in both GEMMs */
 typedef struct ic_plan {
   int kernel;        /* IC_KERNEL_* of the main launch */
   int bm, bn;        /* block tile: output rows (pixels; weight-gradient: G channels) x columns */

@@ -78,15 +78,45 @@ def nonneg(param, minimum=0.0, offset=2.0 ** -18):
 
 
 def gdn(x, gamma_param, beta_param, inverse=False, relu=False,
-        beta_min=1e-6, offset=2.0 ** -18):
+        beta_min=1e-6, offset=2.0 ** -18, bf16_bwd=False):
     """modelling/layers/gdn.py:79-88: y = x / sqrt(conv1x1(x^2, gamma) + beta)
-    (x * sqrt(...) when inverse)."""
+    (x * sqrt(...) when inverse).  bf16_bwd: the backward's two contractions take
+    bf16-rounded operands (_GDNBwdRounded; config C3 emulation, forward GDN only)."""
     if relu:
         x = F.relu(x)
     gamma = nonneg(gamma_param, 0.0, offset)
     beta = nonneg(beta_param, beta_min, offset)
+    if bf16_bwd and not inverse:
+        return _GDNBwdRounded.apply(x, gamma, beta)
     norm = torch.sqrt(F.conv2d(x * x, gamma, beta))
     return x * norm if inverse else x / norm
+
+
+class _GDNBwdRounded(torch.autograd.Function):
+    """y = x * (beta + gamma x^2)^-1/2 with the backward's contractions on bf16-rounded operands:
+    with v = beta + gamma x^2 and q = dL/dv = -1/2 dy x v^-3/2,
+    dx = dy v^-1/2 + 2 x (rnd(q) rnd(gamma)), dgamma = rnd(q)^T rnd(x^2), dbeta = sum q.
+    Not the reference's arithmetic: the emulation of config C3's bf16-operand GDN backward
+    (csrc/gdn_fused.hip, BF); the forward is exact."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta):
+        v = F.conv2d(x * x, gamma, beta)
+        ctx.save_for_backward(x, gamma, v)
+        return x / torch.sqrt(v)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, v = ctx.saved_tensors
+        rs = v.rsqrt()
+        q = -0.5 * dy * x * rs * rs * rs
+        g2 = _rnd(gamma.reshape(gamma.shape[0], gamma.shape[1]))
+        qr = _rnd(q)
+        dxg = torch.einsum("bnhw,nk->bkhw", qr, g2)
+        dx = dy * rs + 2.0 * x * dxg
+        dgamma = torch.einsum("bnhw,bkhw->nk", qr, _rnd(x * x)).reshape(gamma.shape)
+        dbeta = q.sum((0, 2, 3))
+        return dx, dgamma, dbeta
 
 
 def gdn_init(C, gamma_init=0.1, offset=2.0 ** -18):
@@ -119,29 +149,85 @@ def _relu(x, ctl):
     return F.relu(x)
 
 
+# ---------------------------------------------------------------- bf16 operand emulation
+def _rnd(t):
+    """round to bf16 (nearest even) and back: what a bf16-operand GEMM sees of t"""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _ConvRounded(torch.autograd.Function):
+    """A convolution (or transposed convolution) whose forward, input-gradient and
+    weight-gradient GEMMs each take bf16-rounded operands when flagged (rf, rd, rw),
+    accumulated exactly in the working dtype.  Not the reference's arithmetic: the
+    emulation of BASELINE config C3's bf16-operand kernels, so a test can separate the
+    rounding of the operands (a property of the config) from the kernels' own error.
+    With no flag set it equals the plain op."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, opad, transposed, rf, rd, rw):
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, transposed, rd, rw)
+        xi, wi = (_rnd(x), _rnd(w)) if rf else (x, w)
+        if transposed:
+            y = F.conv_transpose2d(xi, wi, b, stride=stride, padding=pad, output_padding=opad)
+        else:
+            y = F.conv2d(xi, wi, b, stride=stride, padding=pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, pad, transposed, rd, rw = ctx.cfg
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            g, wd = (_rnd(gy), _rnd(w)) if rd else (gy, w)
+            dx = (F.conv2d(g, wd, None, stride=stride, padding=pad) if transposed
+                  else torch.nn.grad.conv2d_input(x.shape, wd, g, stride=stride, padding=pad))
+        if ctx.needs_input_grad[1]:
+            g, xw = (_rnd(gy), _rnd(x)) if rw else (gy, x)
+            dw = (torch.nn.grad.conv2d_weight(g, w.shape, xw, stride=stride, padding=pad) if transposed
+                  else torch.nn.grad.conv2d_weight(xw, w.shape, g, stride=stride, padding=pad))
+        db = gy.sum((0, 2, 3)) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def _conv(x, w, b, stride, pad, name, bf16, transposed=False, opad=0):
+    """F.conv2d / F.conv_transpose2d; with `bf16` (a dict: weight name -> (fwd, dgrad, wgrad)
+    flags, and GDN gamma-parameter name -> True for a bf16 backward) the GEMMs flagged for this
+    layer take bf16-rounded operands (_ConvRounded)."""
+    flags = bf16.get(name) if bf16 else None
+    if flags and any(flags):
+        return _ConvRounded.apply(x, w, b, stride, pad, opad, transposed, *flags)
+    if transposed:
+        return F.conv_transpose2d(x, w, b, stride=stride, padding=pad, output_padding=opad)
+    return F.conv2d(x, w, b, stride=stride, padding=pad)
+
+
 # ---------------------------------------------------------------- transforms
-def analysis(P, x, strides=(2, 2, 2, 2), k=5, prefix="analysis_transform.layers."):
+def analysis(P, x, strides=(2, 2, 2, 2), k=5, prefix="analysis_transform.layers.", bf16=None):
     """modelling/blocks/analysis.py:44-71: conv(k, s, pad k//2) with GDN after
-    all but the last conv."""
+    all but the last conv.  bf16: see _conv."""
     n = len(strides)
     for i, s in enumerate(strides):
-        x = F.conv2d(x, P[f"{prefix}{2*i}.weight"], P[f"{prefix}{2*i}.bias"],
-                     stride=s, padding=k // 2)
+        name = f"{prefix}{2*i}.weight"
+        x = _conv(x, P[name], P[f"{prefix}{2*i}.bias"], s, k // 2, name, bf16)
         if i < n - 1:
-            x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"])
+            x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"],
+                    bf16_bwd=bool(bf16 and bf16.get(f"{prefix}{2*i+1}.gamma.param")))
     return x
 
 
-def synthesis(P, x, strides=(2, 2, 2, 2), k=5, prefix="synthesis_transform.layers."):
+def synthesis(P, x, strides=(2, 2, 2, 2), k=5, prefix="synthesis_transform.layers.", bf16=None):
     """modelling/blocks/synthesis.py:44-71: conv_transpose(k, s, pad k//2,
     output_padding s-1) with forward GDN (not IGDN, synthesis.py:65) after all
-    but the last layer."""
+    but the last layer.  bf16: see _conv."""
     n = len(strides)
     for i, s in enumerate(strides):
-        x = F.conv_transpose2d(x, P[f"{prefix}{2*i}.weight"], P[f"{prefix}{2*i}.bias"],
-                               stride=s, padding=k // 2, output_padding=s - 1)
+        name = f"{prefix}{2*i}.weight"
+        x = _conv(x, P[name], P[f"{prefix}{2*i}.bias"], s, k // 2, name, bf16, transposed=True, opad=s - 1)
         if i < n - 1:
-            x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"])
+            x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"],
+                    bf16_bwd=bool(bf16 and bf16.get(f"{prefix}{2*i+1}.gamma.param")))
     return x
 
 
@@ -361,18 +447,20 @@ def ms_ssim_metric_db(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
 # ---------------------------------------------------------------- full model
 def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             loss_names=("MSE",), lam=256.0, ssim_log=True,
-            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None, bin_=1.0):
+            strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None, bin_=1.0,
+            bf16=None):
     """modelling/meta_arch/bmshl2018.py:68-98 Compressor2018.forward.
-    Returns dict of intermediates and the loss dict."""
+    Returns dict of intermediates and the loss dict.  bf16: per-layer bf16 operand
+    emulation of the main transforms' GEMMs (_conv; None = exact)."""
     N, C, H, W = x.shape
     num_pixels = N * H * W
-    y = analysis(P, x, strides)
+    y = analysis(P, x, strides, bf16=bf16)
     z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl)
     z_tilde, p_z, ce_z = factorized(P, z, u_z, train, bin_)
     sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl)
     y_tilde, p_y = conditional(y, sigma, u_y, train, cond, bin_=bin_)
     ce_y = ce_loss(p_y)
-    x_raw = synthesis(P, y_tilde, strides)
+    x_raw = synthesis(P, y_tilde, strides, bf16=bf16)
     x_tilde = lower_bound(upper_bound(x_raw, 1.0), 0.0)
     dist = {}
     for name in loss_names:

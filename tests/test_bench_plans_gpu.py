@@ -20,7 +20,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import HipReluMasks, assert_close, check_relu_ties, rel_err
+from conftest import HipReluMasks, MainLayerIO, assert_close, c3_check, check_relu_ties, rel_err
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -50,14 +50,14 @@ def test_c2_conv_layer(math):
     y = IF.conv2d(xd, wd, b.to(DEV), 2, 2, math=math)
     gy = _r(*y.shape, seed=4).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split_halo", 1: "ig_bf16"}[math]  # split: the halo-reusing kernel at these shapes
+    kern = {2: "ig_split", 1: "ig_bf16"}[math]
     pf = _lib.plan("conv2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
     assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, 128, 1), pf
     assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, 128, 1), pd
-    # weight gradients stay fp32-class in every mode (bf16 runs them split)
-    assert (pw["kernel"], pw["variant"]) == ("wg_split" if math == 2 else "wg_ldsdma", 1), pw
+    # weight gradients: split arithmetic, or bf16 operands on the same two-wave kernel
+    assert (pw["kernel"], pw["variant"]) == ("wg_split" if math == 2 else "wg_bf16", 1), pw
     xr = x.double().requires_grad_(True)
     wr = w.double().requires_grad_(True)
     yr = F.conv2d(xr, wr, b.double(), stride=2, padding=2)
@@ -69,7 +69,10 @@ def test_c2_conv_layer(math):
     else:  # bf16 operands: normwise bar
         assert rel_err(y.detach().cpu(), yr.detach()) < tol
         assert rel_err(xd.grad.cpu(), xr.grad) < tol
-    assert_close(wd.grad.cpu(), wr.grad, 1e-4, "dw")
+    if math == 2:
+        assert_close(wd.grad.cpu(), wr.grad, 1e-4, "dw")
+    else:
+        assert rel_err(wd.grad.cpu(), wr.grad) < tol
 
 
 @pytest.mark.parametrize("math", [2, 1])
@@ -84,13 +87,13 @@ def test_c2_tconv_layer(math):
     y = IF.conv_transpose2d(xd, wd, None, 2, 2, 1, math=math)
     gy = _r(*y.shape, seed=7).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split_halo", 1: "ig_bf16"}[math]  # split: the halo-reusing kernel at these shapes
+    kern = {2: "ig_split", 1: "ig_bf16"}[math]
     pf = _lib.plan("conv_transpose2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv_transpose2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv_transpose2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
     assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, 128, 1), pf
     assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, 128, 1), pd
-    assert pw["kernel"] == ("wg_split" if math == 2 else "wg_ldsdma"), pw
+    assert pw["kernel"] == ("wg_split" if math == 2 else "wg_bf16"), pw
     xr = x.double().requires_grad_(True)
     wr = w.double().requires_grad_(True)
     yr = F.conv_transpose2d(xr, wr, None, stride=2, padding=2, output_padding=1)
@@ -102,7 +105,10 @@ def test_c2_tconv_layer(math):
     else:
         assert rel_err(y.detach().cpu(), yr.detach()) < tol
         assert rel_err(xd.grad.cpu(), xr.grad) < tol
-    assert_close(wd.grad.cpu(), wr.grad, 1e-4, "dw")
+    if math == 2:
+        assert_close(wd.grad.cpu(), wr.grad, 1e-4, "dw")
+    else:
+        assert rel_err(wd.grad.cpu(), wr.grad) < tol
 
 
 # ------------------------------------------------------------------ whole steps per BASELINE config
@@ -158,10 +164,13 @@ def test_config_step_vs_oracle_and_bench_plans(name):
     uz = torch.rand(n, 192, size // 64, size // 64, generator=g)
     uy = torch.rand(n, latent, size // 16, size // 16, generator=g)
     hm = HipReluMasks(model)
+    lio = MainLayerIO(model) if dtype == "bf16" else None
     with IF.record_plans() as log, injected_noise([uz.to(DEV), uy.to(DEV)]):
         xt, losses = model(x.to(DEV))
         losses["total_loss"].backward()
     hm.remove()
+    if lio:
+        lio.remove()
     test_plans = {_key(p) for p in log}
     missing = bench_plans - test_plans
     assert not missing, f"bench kernel instances this test does not reach: {sorted(missing)}"
@@ -170,24 +179,17 @@ def test_config_step_vs_oracle_and_bench_plans(name):
     kw = dict(lam=lam, relu_ctl=ctl)
     if loss == "msssim":
         kw.update(loss_names=("MS_SSIMLoss",), ssim_log=True)
+    if dtype == "bf16":
+        c3_check(model, params, x, uz, uy, xt, losses, hm.masks, log, lam, latent, lio, name)
+        return
     out, ref_losses, ref_grads = ref_cpu.run(params, x, uz, uy, train=True, dtype=torch.float64, **kw)
-    # bf16 operands (C3) move y by ~1e-2 normwise, so h_a's pre-activations differ from the fp64
-    # oracle's by up to ~1e-2 of their range: a mask flip there is a tie at that scale
-    flips = check_relu_ties(hm.masks, ctl, tau=2e-2 if dtype == "bf16" else 1e-4)
+    flips = check_relu_ties(hm.masks, ctl, tau=1e-4)
     errs = {k: rel_err(p.grad.cpu(), ref_grads[k]) for k, p in model.named_parameters()}
     worst = sorted(((e, k) for k, e in errs.items()), reverse=True)[:5]
     print(f"{name}: x_tilde {rel_err(xt.cpu(), out['x_tilde'].detach()):.2e}; ReLU ties {flips}; worst grads {worst}")
-    if dtype == "bf16":
-        # bf16 operands (C3): the SURVEY 8c bf16 bar on outputs and losses; gradients as in test_bf16_gpu
-        assert rel_err(xt.cpu(), out["x_tilde"].detach()) < 1e-2
-        for k in ("total_loss", "bpp", "MSE"):
-            assert abs(float(losses[k]) - float(ref_losses[k])) <= 1e-2 * abs(float(ref_losses[k])), k
-        e = sorted(errs.values())
-        assert e[len(e) // 2] < 1e-2 and e[-1] < 0.15, worst
-        return
     assert_close(xt.cpu(), out["x_tilde"].detach(), 1e-4, "x_tilde")
     for k in ["total_loss", "bpp"] + (["MS_SSIMLoss"] if loss == "msssim" else ["MSE"]):
-        a, b = float(losses[k]), float(ref_losses[k])
+        a, b = float(losses[k].detach()), float(ref_losses[k].detach())
         assert abs(a - b) <= 1e-4 * abs(b), (k, a, b)
     for k, e in errs.items():
         assert e < 1e-4, (k, e, worst)

@@ -18,6 +18,7 @@ for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fus
     | grep -v "not a recognized feature" &
 done
 wait
+ls $B/*.o | wc -l | grep -qx 13 || { echo "abl_build: an object failed to build"; exit 1; }
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libimgcomp.so $B/*.o
 TORCH_DIR=$(python3 -c 'import os, torch; print(os.path.dirname(torch.__file__))')
 g++ -shared -o $O/libimgcomp_torch.so $C/build/torch_ops.o -L$O -limgcomp -L$TORCH_DIR/lib -ltorch -ltorch_cpu -lc10 \
