@@ -64,6 +64,9 @@ MATH_NOTE = {
             "GDN forward, hyperprior and wgrad of maps < 16 wide in fp32_split; entropy models and edges fp32",
 }
 BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
+# configs whose dominant kernel (g_a layer 2 fwd at 32 x 128^2) bench times live: C2 (fp32_split) and
+# C3 (bf16 operands; same layer shape, the latent width does not touch it)
+ROOFLINE_CONFIGS = ("C2", "C3")
 
 
 def _bound_spec(math):
@@ -122,12 +125,14 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
         peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
+    elif math == "bf16":
+        peak, kern = BF16_PEAK_TFLOPS, "ig_kernel_bf16<128,192,64,96> (bf16 operands, fp32 accumulation, 32x32x16 bf16 MFMA)"
     else:
         peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(kern.split(" ")[0]),
-            "peak_note": ("algorithmic fp32 FLOP/s; peak = bf16 dense MFMA 2500 TF / 6 products per fp32 MAC"
-                          if math == "fp32_split" else "fp32 dense MFMA spec"),
+            "peak_note": {"fp32_split": "algorithmic fp32 FLOP/s; peak = bf16 dense MFMA 2500 TF / 6 products per fp32 MAC",
+                          "bf16": "algorithmic FLOP/s; peak = bf16 dense MFMA spec (2500 TF)"}.get(math, "fp32 dense MFMA spec"),
             "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
             "kernel": kern + " + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4),
@@ -233,6 +238,7 @@ def _mfma_peak_measured():
         out["bound_tflops"]["fp32"] = fp32
     if bf16:
         out["bound_tflops"]["fp32_split"] = round(bf16 / 6, 2)
+        out["bound_tflops"]["bf16"] = bf16
     return out
 
 
@@ -316,7 +322,7 @@ def main():
         mode = "hipGraph" + (" + RCCL all-reduce of the flat gradient" if dist else "")
 
     live = None
-    if not args.graph and args.config == "C2" and not args.no_roofline:
+    if not args.graph and args.config in ROOFLINE_CONFIGS and not args.no_roofline:
         core = getattr(model, "module", model)
         live = LiveLaunchTimer(core.analysis_transform.layers[2])
     for _ in range(args.warmup):
@@ -348,7 +354,7 @@ def main():
     value = images / elapsed
     ms = 1e3 * elapsed / args.steps
     roof = None
-    if not args.no_roofline and args.config == "C2":
+    if not args.no_roofline and args.config in ROOFLINE_CONFIGS:
         roof = dominant_kernel_roofline(dev, live_ms=live.ms() if live else None,
                                         live_launches=len(live.pairs) if live else 0, math=conf["math"])
     cpu = None

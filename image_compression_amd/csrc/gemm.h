@@ -55,6 +55,7 @@ struct IgDesc {
   long long Mtot;
   int bm, bn;        // chosen tile (set by ig_plan)
   int bf16;          // bf16 operands, fp32 accumulation (fast path, Cin % 64 == 0); wp holds bf16
+  int dma;           // split tiles of 256 rows on ig_kernel_x3d (set by ig_plan)
   int x3;            // fp32 by exact three-term bf16 split (fast path, Cin % 32 == 0); wp holds three
                      // bf16 planes [part][t][Npad][Cin], part p at wp + p * wplane (bf16 elements)
   long long wplane;

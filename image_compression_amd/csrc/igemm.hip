@@ -739,6 +739,183 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, n0, wm, wn, WM, WN, lane, split);
 }
 
+// ------------------------------------------------------------------ split, every operand by LDS-DMA
+// The split implicit GEMM on 256 x 192 tiles, eight waves of 64 x 96, one block per CU, with
+// no register staging: per K chunk (32 channels of one tap) the block's 256 gathered fp32
+// activation rows (32 KB) and the three pre-split weight planes (36 KB) arrive by LDS-DMA
+// (global_load_lds_dwordx4 from inline asm, so the compiler does not wait for the DMA before
+// LDS reads) into one of two stages; one barrier per chunk publishes chunk c and frees the
+// stage that chunk c + 1's DMA, issued right after it, overwrites.  Each wave splits its own A
+// fragments into three bf16 terms after reading them (8 fp32 per lane per 16-row tile) and runs
+// ig_kernel_x3s's six products per (i, j) in the same order over the same chunk order, so the
+// result is bitwise that kernel's.  Per chunk a 256-row tile stages the weights once for twice
+// the rows of ig_kernel_x3s<128, ...> (68 vs 104 KB per 256 rows), and no VALU or ds_write
+// staging sits between the MFMA phases.
+// fp32 A rows are 128 B (eight 16-B chunks) with the chunks XOR-swizzled by row bits 1 and 3
+// (ig_swa): the four 16-lane groups of a ds_read_b128 fragment read hit distinct bank slots.
+#ifndef IG_X3D
+#define IG_X3D 1
+#endif
+#ifndef IG_X3D_MID
+#define IG_X3D_MID 1  // issue the next chunk's DMA after the A split, between the VALU and the MFMAs (r03p: -1 %)
+#endif
+#ifndef IG_X3D_ABL
+#define IG_X3D_ABL 0  // ablation builds only (tools/abl_build.sh): 1 no DMA after the first chunk, 2 no split
+#endif
+
+// 16 B per lane, global -> LDS at byte offset lds + 16 * lane (wave-uniform lds; M0 restored)
+__device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
+  uint32_t save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+__device__ __forceinline__ int ig_swa(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
+
+__global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
+  constexpr int BM = 256, BN = 192, WM = 64, WN = 96, TM = WM / 16, TN = WN / 16, LDB = 32;
+  constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
+  constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
+  constexpr int STAGE = ASTAGE + BSTAGE;
+  constexpr int NB = 3 * BN / 16;           // 1-KB B DMA pieces per stage (36)
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const IgPhase& P = d.ph[blockIdx.z];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int T = P.T;
+  const int nchunks = T * (d.Cin >> 5);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+
+  // A: wave w DMAs rows 32w + 8k + (lane >> 3), k < 4 (1 KB = 8 rows per piece); lane's
+  // physical chunk lane & 7 holds logical chunk (lane & 7) ^ ig_swa(row)
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[4];
+  int a_iy[4], a_ix[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = 32 * w + 8 * k + (lane >> 3);
+    const uint32_t m = m0 + row;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[k] = (int)gx * d.stride;
+    a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
+               4u * (uint32_t)((lane & 7) ^ ig_swa(row & 15));
+  }
+  // B: wave w DMAs pieces jj = w + 8 kb < 36: plane jj / 12, rows 16 (jj % 12) + (lane >> 2);
+  // lane's physical chunk lane & 3 holds logical chunk (lane & 3) ^ ig_swz(row)
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  uint32_t b_off[5];
+#pragma unroll
+  for (int kb = 0; kb < 5; ++kb) {
+    const int jj = w + 8 * kb;
+    const int q = jj / 12, rb = 16 * (jj - 12 * q) + (lane >> 2);
+    b_off[kb] = (uint32_t)q * (uint32_t)d.wplane + (uint32_t)rb * (uint32_t)d.Cin +
+                8u * (uint32_t)((lane & 3) ^ ig_swz(rb));
+  }
+  const float* __restrict__ xg = d.x;
+  auto issue = [&](int cc, int t, int st) {
+    const uint32_t sb = lbase + (uint32_t)(st * STAGE);
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
+                sb + (uint32_t)((4 * w + k) * 1024));
+    }
+    const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 32);
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) {
+      if (w + 8 * kb < NB) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (w + 8 * kb) * 1024));
+    }
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+  const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
+  const int bch = 8 * (g ^ ig_swz(r));
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  int cn = 0, tn = 0;  // channel chunk and tap of the next chunk to issue
+  if (nchunks > 0) {
+    issue(0, 0, 0);
+    if (++tn == T) { tn = 0; ++cn; }
+  }
+  for (int c = 0; c < nchunks; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!IG_X3D_MID && c + 1 < nchunks && !(IG_X3D_ABL & 1)) {
+      issue(cn, tn, (c + 1) & 1);
+      if (++tn == T) { tn = 0; ++cn; }
+    }
+    const float* As = (const float*)(lds + (c & 1) * STAGE);
+    const __bf16* Bs = (const __bf16*)(lds + (c & 1) * STAGE + ASTAGE);
+    bf16x8 a[3][TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* ar = As + (wm * WM + i * 16 + r) * 32;
+      const floatx4v lo = *(const floatx4v*)(ar + ach0);
+      const floatx4v hi = *(const floatx4v*)(ar + ach1);
+      bf16x4 h0, m0v, l0, h1, m1v, l1;
+      if (IG_X3D_ABL & 2) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        h0 = m0v = l0 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3])});
+        h1 = m1v = l1 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
+      } else {
+      split3_bf16x4(lo, h0, m0v, l0);
+      split3_bf16x4(hi, h1, m1v, l1);
+      }
+      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    if (IG_X3D_MID && c + 1 < nchunks && !(IG_X3D_ABL & 1)) {
+      issue(cn, tn, (c + 1) & 1);
+      if (++tn == T) { tn = 0; ++cn; }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 16 + r) * LDB + bch);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, 0);
+}
+
 // split-K reduction + epilogue: one thread per (row, channel)
 __global__ void ig_reduce_kernel(const IgDesc d) {
   const long long total = d.Mtot * d.Cout;
@@ -834,6 +1011,14 @@ size_t ig_plan(IgDesc& d) {
     // grid, so fewer K splits (and less split-K partial traffic) fill the chip
     d.bm = ((!d.bf16 || IG_BF16_S) && mall < 65536) ? 64 : 128;
     d.bn = 192;
+    // big split maps: 256-row tiles on the all-DMA kernel (one block per CU) where they fill the chip
+    d.dma = 0;
+    if (IG_X3D && d.x3 && !d.bf16 && !d.generic && d.Cout == 192 && d.a_op == AOP_NONE && d.xs_c == 1 &&
+        d.Cin % 32 == 0) {
+      long long t256 = 0;
+      for (int p = 0; p < d.nphase; ++p) t256 += ic_cdiv((long long)d.N * d.ph[p].Hg * d.ph[p].Wg, 256);
+      if (t256 >= 256) { d.bm = 256; d.dma = 1; }
+    }
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
   else { d.bm = 256; d.bn = 32; }
@@ -858,7 +1043,7 @@ size_t ig_plan(IgDesc& d) {
   d.Mtot = mtot;
   // split K when the tile grid cannot fill 256 CUs x 2 blocks
   int ksplit = 1;
-  if (tiles < 512 && nchunks_max >= 4) {
+  if (!d.dma && tiles < 512 && nchunks_max >= 4) {
     ksplit = (int)((1024 + tiles - 1) / tiles);
     int maxs = nchunks_max / 2;
     if (maxs > IG_KSPLIT_MAX) maxs = IG_KSPLIT_MAX;
@@ -877,7 +1062,7 @@ size_t ig_plan(IgDesc& d) {
 
 int ig_kernel_kind(const IgDesc& d) {
   if (d.bf16) return ig_bf16_wide(d) ? IC_KERNEL_IG_BF16 : IC_KERNEL_IG_SPLIT_BF16;
-  if (d.x3) return IC_KERNEL_IG_SPLIT;
+  if (d.x3) return d.dma ? IC_KERNEL_IG_SPLIT_DMA : IC_KERNEL_IG_SPLIT;
   return d.generic ? IC_KERNEL_IG_FP32_GATHER : IC_KERNEL_IG_FP32;
 }
 
@@ -894,6 +1079,14 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.x3 && (d.generic || d.bf16 || d.Cin % 32 != 0 || d.a_op == AOP_ABS || d.bn % 64 != 0)) return IC_ERR_ARG;
   if (d.generic && (d.Kc % 32 != 0)) return IC_ERR_ARG;
   int rc;
+  if (d.dma) {
+    int mt = 0;
+    for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
+    if (d.ksplit != 1 || d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
+    hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase), dim3(512), 0, s, d);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
   else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);

@@ -191,6 +191,7 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
 /* 19: retired (a halo-reusing split kernel, measured slower) */
 #define IC_KERNEL_WG_BF16 20        /* wg_x3d_kernel with bf16 operands (one product), fp32 accumulation */
 #define IC_KERNEL_GDN_FUSED_BF16 21 /* gdn_bwd_fused_kernel with bf16 operands in both GEMMs */
+#define IC_KERNEL_IG_SPLIT_DMA 22   /* ig_kernel_x3d: split arithmetic, 256-row tiles, operands by LDS-DMA */
 typedef struct ic_plan {
   int kernel;        /* IC_KERNEL_* of the main launch */
   int bm, bn;        /* block tile: output rows (pixels; weight-gradient: G channels) x columns */

@@ -148,10 +148,10 @@ def test_plan_query_c2_instances():
     from image_compression_amd import _lib
     x, y = _act(32, 192, 128, 128), _act(32, 192, 64, 64)
     p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 2)
-    assert (p["kernel"], p["bm"], p["bn"], p["ksplit"]) == ("ig_split", 128, 192, 1)
-    assert p["blocks"] == 32 * 64 * 64 // 128
+    assert (p["kernel"], p["bm"], p["bn"], p["ksplit"]) == ("ig_split_dma", 256, 192, 1)
+    assert p["blocks"] == 32 * 64 * 64 // 256
     p = _lib.plan("conv2d_dgrad", y, x, 5, 2, 2, 2)
-    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split", 128, 1)
+    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split_dma", 256, 1)
     # 32 k output pixels: 64-row tiles (512 of them: no split K)
     p = _lib.plan("conv2d_fwd", _act(8, 192, 128, 128), _act(8, 192, 64, 64), 5, 2, 2, 2)
     assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split", 64, 1)

@@ -50,12 +50,12 @@ def test_c2_conv_layer(math):
     y = IF.conv2d(xd, wd, b.to(DEV), 2, 2, math=math)
     gy = _r(*y.shape, seed=4).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split", 1: "ig_bf16"}[math]
+    kern, bm = {2: ("ig_split_dma", 256), 1: ("ig_bf16", 128)}[math]
     pf = _lib.plan("conv2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
-    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, 128, 1), pf
-    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, 128, 1), pd
+    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, bm, 1), pf
+    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, bm, 1), pd
     # weight gradients: split arithmetic, or bf16 operands on the same two-wave kernel
     assert (pw["kernel"], pw["variant"]) == ("wg_split" if math == 2 else "wg_bf16", 1), pw
     xr = x.double().requires_grad_(True)
@@ -87,12 +87,12 @@ def test_c2_tconv_layer(math):
     y = IF.conv_transpose2d(xd, wd, None, 2, 2, 1, math=math)
     gy = _r(*y.shape, seed=7).to(DEV).contiguous(memory_format=CL)
     y.backward(gy)
-    kern = {2: "ig_split", 1: "ig_bf16"}[math]
+    kern, bm = {2: ("ig_split_dma", 256), 1: ("ig_bf16", 128)}[math]
     pf = _lib.plan("conv_transpose2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv_transpose2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv_transpose2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
-    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, 128, 1), pf
-    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, 128, 1), pd
+    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, bm, 1), pf
+    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, bm, 1), pd
     assert pw["kernel"] == ("wg_split" if math == 2 else "wg_bf16"), pw
     xr = x.double().requires_grad_(True)
     wr = w.double().requires_grad_(True)

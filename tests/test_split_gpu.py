@@ -164,7 +164,7 @@ def test_model_fp32_split_vs_oracle():
     check_relu_ties(hm.masks, ctl)
     assert_close(xt.cpu(), out["x_tilde"].detach(), 1e-4, "x_tilde")
     for k in ("total_loss", "bpp", "MSE"):
-        a, b = float(losses[k]), float(ref_losses[k])
+        a, b = float(losses[k].detach()), float(ref_losses[k].detach())
         assert abs(a - b) <= 1e-4 * abs(b), (k, a, b)
     for name, p in model.named_parameters():
         assert rel_err(p.grad.cpu(), ref_grads[name]) < 1e-4, name

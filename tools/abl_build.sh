@@ -10,7 +10,7 @@ C=$R/image_compression_amd/csrc
 B=$R/tools/_abl/build_$TAG
 O=$R/tools/_abl/$TAG
 mkdir -p $B $O
-NOPK_SRCS=${NOPK_SRCS-"entropy elementwise msssim metrics optim"}   # as the Makefile (override: NOPK_SRCS=...)
+NOPK_SRCS=${NOPK_SRCS-"entropy elementwise msssim metrics optim igemm"}   # as the Makefile (override: NOPK_SRCS=...)
 for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics; do
   extra=""
   case " $NOPK_SRCS " in *" $f "*) extra="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
