@@ -124,7 +124,8 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
     pm = _mfma_peak_measured()
     if math == "fp32_split":
         # every fp32 MAC costs six bf16 MACs: the bound is the bf16 MFMA peak / 6
-        peak, kern = BF16_PEAK_TFLOPS / 6, "ig_kernel_x3s<128,192,64,96,3> (fp32 by 3-term bf16 split, 16x16x32 bf16 MFMA)"
+        peak, kern = BF16_PEAK_TFLOPS / 6, ("ig_kernel_x3d (256x192 tiles, operands by LDS-DMA; fp32 by 3-term bf16 "
+                                           "split, 16x16x32 bf16 MFMA)")
     elif math == "bf16":
         peak, kern = BF16_PEAK_TFLOPS, "ig_kernel_bf16<128,192,64,96> (bf16 operands, fp32 accumulation, 32x32x16 bf16 MFMA)"
     else:

@@ -756,6 +756,9 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D
 #define IG_X3D 1
 #endif
+#ifndef IG_X3D_MINT
+#define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
+#endif
 #ifndef IG_X3D_MID
 #define IG_X3D_MID 1  // issue the next chunk's DMA after the A split, between the VALU and the MFMAs (r03p: -1 %)
 #endif
@@ -787,7 +790,10 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   constexpr int NB = 3 * BN / 16;           // 1-KB B DMA pieces per stage (36)
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
-  const IgPhase& P = d.ph[blockIdx.z];
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
   uint32_t bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
   if ((int)bx >= P.mtiles) return;
@@ -795,6 +801,9 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   const uint32_t m0 = bx * BM;
   const int T = P.T;
   const int nchunks = T * (d.Cin >> 5);
+  // split K: chunks [cb, ce) of this block's split (a split past the phase's chunks adds zeros)
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(
@@ -860,20 +869,20 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 
-  int cn = 0, tn = 0;  // channel chunk and tap of the next chunk to issue
-  if (nchunks > 0) {
-    issue(0, 0, 0);
+  int cn = cb / T, tn = cb - (cb / T) * T;  // channel chunk and tap of the next chunk to issue
+  if (cb < ce) {
+    issue(cn, tn, 0);
     if (++tn == T) { tn = 0; ++cn; }
   }
-  for (int c = 0; c < nchunks; ++c) {
+  for (int c = cb; c < ce; ++c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!IG_X3D_MID && c + 1 < nchunks && !(IG_X3D_ABL & 1)) {
-      issue(cn, tn, (c + 1) & 1);
+    if (!IG_X3D_MID && c + 1 < ce && !(IG_X3D_ABL & 1)) {
+      issue(cn, tn, (c + 1 - cb) & 1);
       if (++tn == T) { tn = 0; ++cn; }
     }
-    const float* As = (const float*)(lds + (c & 1) * STAGE);
-    const __bf16* Bs = (const __bf16*)(lds + (c & 1) * STAGE + ASTAGE);
+    const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
+    const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
     bf16x8 a[3][TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -893,8 +902,8 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
       a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
     }
-    if (IG_X3D_MID && c + 1 < nchunks && !(IG_X3D_ABL & 1)) {
-      issue(cn, tn, (c + 1) & 1);
+    if (IG_X3D_MID && c + 1 < ce && !(IG_X3D_ABL & 1)) {
+      issue(cn, tn, (c + 1 - cb) & 1);
       if (++tn == T) { tn = 0; ++cn; }
     }
 #pragma unroll
@@ -913,7 +922,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       }
     }
   }
-  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, 0);
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
 }
 
 // split-K reduction + epilogue: one thread per (row, channel)
@@ -1017,7 +1026,9 @@ size_t ig_plan(IgDesc& d) {
         d.Cin % 32 == 0) {
       long long t256 = 0;
       for (int p = 0; p < d.nphase; ++p) t256 += ic_cdiv((long long)d.N * d.ph[p].Hg * d.ph[p].Wg, 256);
-      if (t256 >= 256) { d.bm = 256; d.dma = 1; }
+      // K split (below 256 tiles) only for one-phase maps: the phases of a transposed conv have
+      // 9 / 6 / 6 / 4 taps, so equal chunk ranges leave one block per CU waiting on the longest
+      if (t256 >= 256 || (d.nphase == 1 && t256 >= IG_X3D_MINT)) { d.bm = 256; d.dma = 1; }
     }
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
@@ -1043,7 +1054,13 @@ size_t ig_plan(IgDesc& d) {
   d.Mtot = mtot;
   // split K when the tile grid cannot fill 256 CUs x 2 blocks
   int ksplit = 1;
-  if (!d.dma && tiles < 512 && nchunks_max >= 4) {
+  if (d.dma && tiles < 256 && nchunks_max >= 4) {  // one block per CU
+    ksplit = (int)((256 + tiles - 1) / tiles);
+    int maxs = nchunks_max / 2;
+    if (maxs > IG_KSPLIT_MAX) maxs = IG_KSPLIT_MAX;
+    if (ksplit > maxs) ksplit = maxs;
+    if (ksplit < 1) ksplit = 1;
+  } else if (!d.dma && tiles < 512 && nchunks_max >= 4) {
     ksplit = (int)((1024 + tiles - 1) / tiles);
     int maxs = nchunks_max / 2;
     if (maxs > IG_KSPLIT_MAX) maxs = IG_KSPLIT_MAX;
@@ -1082,12 +1099,12 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (d.dma) {
     int mt = 0;
     for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
-    if (d.ksplit != 1 || d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
-    hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase), dim3(512), 0, s, d);
+    if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
+    hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     IC_CHECK_LAUNCH();
-    return IC_OK;
+    rc = IC_OK;
   }
-  if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
+  else if (d.bn == 192 && d.bm == 64) rc = ig_launch_t<64, 192, 32, 96>(d, s);
   else if (d.bn == 192) rc = ig_launch_t<128, 192, 64, 96>(d, s);
   else if (d.bn == 64) rc = ig_launch_t<128, 64, 64, 32>(d, s);
   else rc = ig_launch_t<256, 32, 64, 32>(d, s);

@@ -152,9 +152,12 @@ def test_plan_query_c2_instances():
     assert p["blocks"] == 32 * 64 * 64 // 256
     p = _lib.plan("conv2d_dgrad", y, x, 5, 2, 2, 2)
     assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split_dma", 256, 1)
-    # 32 k output pixels: 64-row tiles (512 of them: no split K)
+    # 32 k output pixels: 128 tiles of 256 rows, K split in 2 to fill the chip
     p = _lib.plan("conv2d_fwd", _act(8, 192, 128, 128), _act(8, 192, 64, 64), 5, 2, 2, 2)
-    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split", 64, 1)
+    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_split_dma", 256, 2)
+    # ... but a transposed conv's four unequal phases stay on 64-row tiles
+    p = _lib.plan("conv_transpose2d_fwd", _act(32, 192, 16, 16), _act(32, 192, 32, 32), 5, 2, 2, 2)
+    assert (p["kernel"], p["bm"]) == ("ig_split", 64)
     p = _lib.plan("conv2d_wgrad", x, y, 5, 2, 2, 2)
     assert (p["kernel"], p["variant"]) == ("wg_split", 1) and p["nsplit"] >= 1
     p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 0)
@@ -164,6 +167,8 @@ def test_plan_query_c2_instances():
     # small maps: 64-row tiles with split-K
     p = _lib.plan("conv2d_fwd", _act(32, 192, 16, 16), _act(32, 192, 8, 8), 5, 2, 2, 2)
     assert (p["kernel"], p["bm"]) == ("ig_split", 64) and p["ksplit"] > 1
+    p = _lib.plan("conv2d_fwd", _act(32, 192, 32, 32), _act(32, 192, 16, 16), 5, 2, 2, 2)
+    assert (p["kernel"], p["bm"]) == ("ig_split_dma", 256) and p["ksplit"] == 8
     # image edges and GDN
     img = _act(32, 3, 256, 256, cl=False)
     assert _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 2)["kernel"] == "edge_conv"

@@ -117,7 +117,7 @@ CONFIGS = {
     "C2": (32, 32, 256, "fp32_split", 192, "mse", 256.0),
     "C3": (32, 32, 256, "bf16", 320, "mse", 4096.0),
     "C4": (16, 16, 256, "fp32_split", 192, "msssim", 64.0),
-    "C5": (16, 4, 512, "fp32_split", 192, "mse", 8192.0),
+    "C5": (16, 16, 512, "fp32_split", 192, "mse", 8192.0),  # the bench batch: tile choices depend on it
 }
 
 

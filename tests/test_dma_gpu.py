@@ -84,3 +84,33 @@ def test_dma_tconv_fwd_dgrad():
     dxn = ops.conv_transpose2d_dgrad(gy, w, x, 2, 2, 0)
     dxr = F.conv2d(gy.double(), w.double(), None, stride=2, padding=2)
     _check(dxs, dxn, dxr, "dx")
+
+
+# K split across blocks (fewer than 256 tiles of 256 rows, one-phase convs): 8 x 32^2 -> ksplit 8,
+# 8 x 64^2 -> 2, 13 x 25^2 (ragged, 32 tiles) -> 8; the partial sums reduced in fixed order
+@pytest.mark.parametrize("n,h,ksplit", [(8, 64, 8), (8, 128, 2), (13, 50, 8)])
+def test_dma_split_k(n, h, ksplit):
+    from image_compression_amd import _lib, functional as IF
+    ops = _lib.ops()
+    x = _r(n, 192, h, h, seed=21).contiguous(memory_format=CL)
+    w = _r(192, 192, 5, 5, seed=22, scale=0.03)
+    b = _r(192, seed=23, scale=0.1)
+    ho = (h + 4 - 5) // 2 + 1
+    y = torch.empty(n, 192, ho, ho, device=DEV).contiguous(memory_format=CL)
+    assert _plan("conv2d_fwd", x, y, 5, 2, 2) == ("ig_split_dma", 256, ksplit)
+    with torch.no_grad():
+        ys = IF.conv2d(x, w, b, 2, 2, math=2)
+        yn = IF.conv2d(x, w, b, 2, 2, math=0)
+        yr = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=2)
+    _check(ys, yn, yr, "y")
+    # deterministic: the same launch twice is bitwise equal
+    with torch.no_grad():
+        assert torch.equal(ys, IF.conv2d(x, w, b, 2, 2, math=2))
+    # a 3x3 stride-1 conv (h_a.0's shape class)
+    x1 = _r(n, 192, ho, ho, seed=24).contiguous(memory_format=CL)
+    y1 = torch.empty(n, 192, ho, ho, device=DEV).contiguous(memory_format=CL)
+    if _plan("conv2d_fwd", x1, y1, 3, 1, 1)[0] == "ig_split_dma":
+        with torch.no_grad():
+            _check(IF.conv2d(x1, w[:, :, :3, :3].contiguous(), b, 1, 1, math=2),
+                   IF.conv2d(x1, w[:, :, :3, :3].contiguous(), b, 1, 1, math=0),
+                   F.conv2d(x1.double(), w[:, :, :3, :3].double(), b.double(), stride=1, padding=1), "y3x3")
