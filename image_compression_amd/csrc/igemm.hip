@@ -759,12 +759,6 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
 #endif
-#ifndef IG_X3D_MID
-#define IG_X3D_MID 1  // issue the next chunk's DMA after the A split, between the VALU and the MFMAs (r03p: -1 %)
-#endif
-#ifndef IG_X3D_ABL
-#define IG_X3D_ABL 0  // ablation builds only (tools/abl_build.sh): 1 no DMA after the first chunk, 2 no split
-#endif
 
 // 16 B per lane, global -> LDS at byte offset lds + 16 * lane (wave-uniform lds; M0 restored)
 __device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
@@ -877,10 +871,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   for (int c = cb; c < ce; ++c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!IG_X3D_MID && c + 1 < ce && !(IG_X3D_ABL & 1)) {
-      issue(cn, tn, (c + 1 - cb) & 1);
-      if (++tn == T) { tn = 0; ++cn; }
-    }
     const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
     const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
     bf16x8 a[3][TM];
@@ -890,19 +880,14 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       const floatx4v lo = *(const floatx4v*)(ar + ach0);
       const floatx4v hi = *(const floatx4v*)(ar + ach1);
       bf16x4 h0, m0v, l0, h1, m1v, l1;
-      if (IG_X3D_ABL & 2) {
-        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-        h0 = m0v = l0 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3])});
-        h1 = m1v = l1 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
-      } else {
       split3_bf16x4(lo, h0, m0v, l0);
       split3_bf16x4(hi, h1, m1v, l1);
-      }
       a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
       a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
       a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
     }
-    if (IG_X3D_MID && c + 1 < ce && !(IG_X3D_ABL & 1)) {
+    // the next chunk's DMA, between the split (VALU) and the MFMAs (r03p: 1 % faster than before the split)
+    if (c + 1 < ce) {
       issue(cn, tn, (c + 1 - cb) & 1);
       if (++tn == T) { tn = 0; ++cn; }
     }
