@@ -218,15 +218,23 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 }
 
 // ------------------------------------------------------------------ conv, split
-// IC_MATH_SPLIT: fp32 by the exact three-term bf16 split on
-// v_mfma_f32_16x16x32_bf16 (six products per MAC, 3/8 of the fp32 MFMA's
-// cycles), T*C <= 96 (three 32-wide k-steps).  The weights, split, sit in LDS
-// as A fragments [part][s][n][32] (16-B chunks XOR (n & 3)): 110 KB, so one
-// block of 8 waves per CU; wave w owns channel slice w & 3 and m-tiles
-// 2 (w >> 2), +1 of every unit.  B fragments (8 consecutive k of one pixel)
-// are gathered from the fp32 patch by the per-lane offset table and split in
-// registers.  The patch pipeline (waves 0-3) and the epilogue are edge_conv's.
+// IC_MATH_SPLIT: fp32 by the exact three-term bf16 split on v_mfma_f32_16x16x32_bf16
+// (six products per MAC), T*C <= 96 (three 32-wide k-steps).  One block of 8 waves per CU;
+// wave w owns channel slice w & 3 (its split weights held as A fragments in 108 VGPRs for the
+// launch) and m-tiles 2 (w >> 2), +1 of every unit.  The B operand of unit u — im2col of its
+// patch, [pixel 64][k 96], split into three bf16 planes — is built once per unit by all 512
+// threads (four consecutive k of one pixel per thread and pass: four patch reads, one paired
+// split, three 8-B stores) one unit ahead of the MFMAs, into two plane buffers (16-B chunks
+// XOR 2 on pixels with bit 3 set: conflict-free fragment reads), so each fragment is three
+// ds_read_b128 and the split is done once per value instead of once per wave and tap that
+// reads it (the per-wave gather-and-split cost 0.12 of 0.20 ms, r03zb; now 0.17 ms).
+// Patches run two units ahead of the MFMAs (waves 0-3 load them into registers and store them
+// into two patch buffers); one barrier per unit.  The output leaves in one burst per unit after
+// the MFMAs: streaming it out under them (one store per MFMA group, or two 4-wave blocks per CU
+// drifting apart, or waves 4-7 storing a phase late) measured slower (r03zf-r03zj).
 constexpr int EC3_S = 3;
+constexpr int EC3_KP = 32 * EC3_S;       // k columns of the B planes (96)
+constexpr int EC3_PL = SEG * EC3_KP;     // bf16 per plane
 template <int COUT>
 __global__ void __launch_bounds__(512, 1)
     edge_conv_x3_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
@@ -234,9 +242,9 @@ __global__ void __launch_bounds__(512, 1)
   typedef __bf16 eb4 __attribute__((ext_vector_type(4)));
   typedef __bf16 eb8 __attribute__((ext_vector_type(8)));
   constexpr int NTW = COUT / 64;
-  constexpr int PLANE = EC3_S * COUT * 32;  // bf16 per part
-  __shared__ __attribute__((aligned(16))) __bf16 wl[3 * PLANE];
-  __shared__ __attribute__((aligned(16))) float lds[2 * (PMAX + 2 * SEG * 2)];
+  __shared__ __attribute__((aligned(16))) __bf16 bpl[2 * 3 * EC3_PL];  // two units' B planes
+  __shared__ __attribute__((aligned(16))) float lds[2 * (PMAX + 2 * SEG * 2)];  // two patches
+  __shared__ __attribute__((aligned(16))) float bl[COUT];  // bias (read per unit: frees 4 NTW VGPRs)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int nbase = (w & 3) * (COUT / 4);
@@ -247,55 +255,83 @@ __global__ void __launch_bounds__(512, 1)
   const int zero_off = PSZ;
   const int bufsz = PMAX + 2 * SEG * 2;
 
-  for (int i = tid; i < EC3_S * COUT * 32; i += 512) {
-    const int kk = i & 31, n = (i >> 5) % COUT, sx = (i >> 5) / COUT;
-    const int kq = 32 * sx + kk;
-    const float v = (sx < S && kq < Kp) ? wp[(size_t)n * Kp + kq] : 0.f;
-    __bf16 hh, mm, ll;
-    split3_bf16(v, hh, mm, ll);
-    const int o = (sx * COUT + n) * 32 + (((kk >> 3) ^ (n & 3)) << 3) + (kk & 7);
-    wl[o] = hh;
-    wl[PLANE + o] = mm;
-    wl[2 * PLANE + o] = ll;
-  }
-  int koff[EC3_S][8];
+  // split weights as A fragments: aw[part][sx][j] = plane part of wp[n = nbase + 16 j + li][32 sx + 8 lq .. + 7]
+  eb8 aw[3][EC3_S][NTW];
 #pragma unroll
   for (int sx = 0; sx < EC3_S; ++sx)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) koff[sx][e] = edge_koff(g, 32 * sx + 8 * lq + e, zero_off, zero_off, false);
-  floatx4v bv[NTW];
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
-  for (int j = 0; j < NTW; ++j)
+      for (int e = 0; e < 8; ++e) {
+        const int kq = 32 * sx + 8 * lq + e;
+        const float v = (sx < S && kq < Kp) ? wp[(size_t)(nbase + 16 * j + li) * Kp + kq] : 0.f;
+        __bf16 hh, mm, ll;
+        split3_bf16(v, hh, mm, ll);
+        aw[0][sx][j][e] = hh;
+        aw[1][sx][j][e] = mm;
+        aw[2][sx][j][e] = ll;
+      }
+  // plane build assignment: groups gi = tid + 512 q (q < 3) = (pixel gi / 24, k quad gi % 24)
+  int bkoff[3][4], bdst[3];  // patch offsets of the group's 4 k at its pixel; plane offset
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[j][r] = bias ? bias[nbase + 16 * j + 4 * lq + r] : 0.f;
+  for (int q = 0; q < 3; ++q) {
+    const int gi = tid + 512 * q;
+    const int p = gi / 24, kq = gi - 24 * (gi / 24);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bkoff[q][e] = edge_koff(g, 4 * kq + e, zero_off, zero_off, false) + g.stride * p;
+    const int c16 = kq >> 1;
+    bdst[q] = p * EC3_KP + 8 * (c16 ^ (((p >> 3) & 1) << 1)) + 4 * (kq & 1);
+  }
+  for (int i = tid; i < COUT; i += 512) bl[i] = bias ? bias[i] : 0.f;
   for (int i = tid; i < 2 * SEG * 2; i += 512) {
     lds[PSZ + i] = 0.f;
     lds[bufsz + PSZ + i] = 0.f;
   }
+  auto build = [&](const float* patch, __bf16* planes) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const floatx4v x = {patch[bkoff[q][0]], patch[bkoff[q][1]], patch[bkoff[q][2]], patch[bkoff[q][3]]};
+      eb4 h, m, l;
+      split3_bf16x4(x, h, m, l);
+      *(eb4*)(planes + bdst[q]) = h;
+      *(eb4*)(planes + EC3_PL + bdst[q]) = m;
+      *(eb4*)(planes + 2 * EC3_PL + bdst[q]) = l;
+    }
+  };
 
   EdgePatchMap pm;
   edge_patch_map(g, pm, tid & 255);
-  long long u = blockIdx.x;
-  int buf = 0;
+  const long long u0 = blockIdx.x, gs = gridDim.x;
   float pr[PREG];
-  if (u < g.units && stager) {
-    edge_patch_load(g, pm, u, pr);
+  // prologue: patch(u0) -> buffer 0, planes(u0) -> plane buffer 0, patch(u0 + gs) -> buffer 1
+  if (u0 < g.units && stager) {
+    edge_patch_load(g, pm, u0, pr);
     edge_patch_store(g, pr, lds, tid);
+  }
+  __syncthreads();
+  if (u0 < g.units) build(lds, bpl);
+  if (u0 + gs < g.units && stager) {
+    edge_patch_load(g, pm, u0 + gs, pr);
+    edge_patch_store(g, pr, lds + bufsz, tid);
   }
   floatx4v ob[2][NTW];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) ob[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-  for (; u < g.units; u += gridDim.x) {
+  int it = 0;
+  for (long long u = u0; u < g.units; u += gs, ++it) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) asm volatile("" ::"v"(ob[t][j]));  // keeps `ob` apart from `acc`
-    __syncthreads();  // patch `buf` (and the weights) complete; everyone is done with buf^1
-    const long long un = u + gridDim.x;
-    if (un < g.units && stager) edge_patch_load(g, pm, un, pr);
-    const float* patch = lds + buf * bufsz;
+    // planes(u) and patch(u + gs) are in LDS; every read of plane buffer (it + 1) & 1 and patch
+    // buffer it & 1 (the previous iteration's) is done
+    __syncthreads();
+    const long long u1 = u + gs, u2 = u + 2 * gs;
+    if (u2 < g.units && stager) edge_patch_load(g, pm, u2, pr);
+    if (u1 < g.units) build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);
+    const __bf16* planes = bpl + (it & 1) * 3 * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -304,69 +340,51 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int sx = 0; sx < EC3_S; ++sx) {
       if (sx < S) {
-        eb8 aw[3][NTW];
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int n = nbase + 16 * j + li;
-          const int o = (sx * COUT + n) * 32 + ((lq ^ (n & 3)) << 3);
-#pragma unroll
-          for (int q = 0; q < 3; ++q) aw[q][j] = *(const eb8*)(wl + q * PLANE + o);
-        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const int m = 16 * (mt0 + t) + li;
-          float v[8];
+          const int p = 16 * (mt0 + t) + li;
+          const int off = p * EC3_KP + 8 * ((4 * sx + lq) ^ (((p >> 3) & 1) << 1));
+          eb8 bf[3];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = patch[koff[sx][e] + g.stride * m];
-          eb4 h0, m0, l0, h1, m1, l1;
-          split3_bf16x4(floatx4v{v[0], v[1], v[2], v[3]}, h0, m0, l0);
-          split3_bf16x4(floatx4v{v[4], v[5], v[6], v[7]}, h1, m1, l1);
-          const eb8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-          const eb8 bm = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
-          const eb8 bl = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+          for (int q = 0; q < 3; ++q) bf[q] = *(const eb8*)(planes + q * EC3_PL + off);
+          // the six products, smallest first (a dependent MFMA issues back to back)
+          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-          for (int j = 0; j < NTW; ++j) {
-            floatx4v& c = acc[t][j];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[2][j], bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][j], bm, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bl, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][j], bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bm, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][j], bh, c, 0, 0, 0);
-          }
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int pr6 = 0; pr6 < 6; ++pr6)
+              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[PA[pr6]][sx][j], bf[PB[pr6]], acc[t][j], 0, 0, 0);
         }
       }
     }
-    // the next patch into the free buffer before the epilogue's global stores:
-    // waiting for its loads then never waits for stores (vmcnt counts both)
-    if (un < g.units && stager) edge_patch_store(g, pr, lds + (buf ^ 1) * bufsz, tid);
-    // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li)
-    const int seg = (int)(u % g.units_per_row);
-    const long long rr = u / g.units_per_row;
-    const int oy = (int)(rr % g.Ho);
-    const int n = (int)(rr / g.Ho);
-    const int ox0 = seg * SEG;
-    float* yb = y + n * ys_n + (long long)oy * ys_h + nbase + 4 * lq;
-    // the stored values stay in registers of their own (`ob`, live across the
-    // unit loop): overwriting a store's data registers waits for the store
+    // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration),
+    // before this unit's global stores: waiting for its loads then never waits for them
+    if (u2 < g.units && stager) edge_patch_store(g, pr, lds + (it & 1) * bufsz, tid);
+    // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li).  The stored values
+    // stay in registers of their own (`ob`, live across the unit loop): overwriting a store's data
+    // registers waits for the store
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < NTW; ++j) {
+      const floatx4v bv = *(const floatx4v*)(bl + nbase + 16 * j + 4 * lq);
 #pragma unroll
-      for (int j = 0; j < NTW; ++j)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float v = acc[t][j][r] + bv[j][r];
-          ob[t][j][r] = (relu && !(v > 0.f)) ? 0.f : v;  // branch-free ReLU
+          const float x = acc[t][j][r] + bv[r];
+          ob[t][j][r] = (relu && !(x > 0.f)) ? 0.f : x;  // branch-free ReLU
         }
+    }
+    const int seg = (int)(u % g.units_per_row);
+    const long long rr = u / g.units_per_row;
+    float* yb = y + (rr / g.Ho) * ys_n + (rr % g.Ho) * ys_h + nbase + 4 * lq;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int ox = ox0 + 16 * (mt0 + t) + li;
+      const int ox = seg * SEG + 16 * (mt0 + t) + li;
       if (ox < g.Wo) {
 #pragma unroll
         for (int j = 0; j < NTW; ++j) *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = ob[t][j];
       }
     }
-    buf ^= 1;
   }
 }
 
