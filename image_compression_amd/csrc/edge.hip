@@ -59,48 +59,63 @@ struct EdgeGeom {
 // the patch of unit u: patch[(c*k + ky)*PW + j] = x[n][c][iy0+ky][ix0+j] (0 outside
 // the image).  Loaded into registers first (pr) and written to LDS later, so
 // the global-load latency hides behind the current unit's MFMAs.
-constexpr int PREG = (PMAX + 255) / 256;
+constexpr int PREG = (PMAX + 255) / 256;  // per thread of a 256-thread stager
 
-// This thread's patch elements i = tid + 256 q, decomposed once per launch
+// This thread's patch elements i = tid + NT q (NT stager threads), decomposed once per launch
 // (the divisions by the runtime patch width and kernel size are not redone
 // per unit) and packed into one register each: (c << 12) | (ky << 9) | j, or
 // -1 for i >= C*k*PW.
-struct EdgePatchMap {
-  int pk[PREG];
+template <int NT = 256>
+struct EdgePatchMapT {
+  static constexpr int R = (PMAX + NT - 1) / NT;
+  int pk[R];
 };
-__device__ __forceinline__ void edge_patch_map(const EdgeGeom& g, EdgePatchMap& m, int tid) {
+typedef EdgePatchMapT<256> EdgePatchMap;
+template <int NT>
+__device__ __forceinline__ void edge_patch_map(const EdgeGeom& g, EdgePatchMapT<NT>& m, int tid) {
   const int tot = g.C * g.k * g.PW;
 #pragma unroll
-  for (int q = 0; q < PREG; ++q) {
-    const int i = tid + 256 * q;
+  for (int q = 0; q < EdgePatchMapT<NT>::R; ++q) {
+    const int i = tid + NT * q;
     const int row = i / g.PW, j = i - (i / g.PW) * g.PW;
     const int c = row / g.k, ky = row - (row / g.k) * g.k;
     m.pk[q] = i < tot ? (c << 12) | (ky << 9) | j : -1;
   }
 }
-__device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, const EdgePatchMap& m, long long u,
-                                                float (&pr)[PREG]) {
-  const int seg = (int)(u % g.units_per_row);
-  const long long r = u / g.units_per_row;
-  const int oy = (int)(r % g.Ho);
-  const int n = (int)(r / g.Ho);
+// Branch-free (every lane loads and stores; out-of-image elements load the zero page, elements
+// past the patch store their zero onto its first zero-run slot): with no exec-masked memory
+// operations, and called unconditionally, the waitcnt pass tracks the loads exactly instead of
+// waiting (vmcnt) at the loop head for everything in flight, the previous unit's output stores
+// included (r03zl).  Unit and image offsets in 32 bits (edge_geom bounds them).
+template <int NT>
+__device__ __forceinline__ void edge_patch_load(const EdgeGeom& g, const EdgePatchMapT<NT>& m, long long u,
+                                                float (&pr)[EdgePatchMapT<NT>::R]) {
+  const unsigned uu = (unsigned)u, upr = (unsigned)g.units_per_row, ho = (unsigned)g.Ho;
+  const unsigned r = uu / upr;
+  const int seg = (int)(uu - r * upr);
+  const unsigned n = r / ho;
+  const int oy = (int)(r - n * ho);
   const int iy0 = oy * g.stride - g.pad, ix0 = seg * SEG * g.stride - g.pad;
-  const float* xb = g.x + n * g.sn;
+  const float* xb = g.x + (long long)n * g.sn;
+  const int sc = (int)g.sc, sh = (int)g.sh;
 #pragma unroll
-  for (int q = 0; q < PREG; ++q) {
+  for (int q = 0; q < EdgePatchMapT<NT>::R; ++q) {
     const int pk = m.pk[q];
     const int iy = iy0 + ((pk >> 9) & 7), ix = ix0 + (pk & 511);
     const bool ok = pk >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    pr[q] = ok ? xb[(long long)(pk >> 12) * g.sc + (long long)iy * g.sh + ix] : 0.f;
+    const int off = (pk >> 12) * sc + iy * sh + ix;
+    pr[q] = *(ok ? xb + off : (const float*)edge_zero_page);  // no use of the value before the store
   }
 }
 
-__device__ __forceinline__ void edge_patch_store(const EdgeGeom& g, const float (&pr)[PREG], float* patch, int tid) {
+template <int NT = 256>
+__device__ __forceinline__ void edge_patch_store(const EdgeGeom& g, const float (&pr)[EdgePatchMapT<NT>::R],
+                                                 float* patch, int tid) {
   const int tot = g.C * g.k * g.PW;
 #pragma unroll
-  for (int q = 0; q < PREG; ++q) {
-    const int i = tid + 256 * q;
-    if (i < tot) patch[i] = pr[q];
+  for (int q = 0; q < EdgePatchMapT<NT>::R; ++q) {
+    const int i = tid + NT * q;
+    patch[i < tot ? i : tot] = pr[q];  // pr = 0 past the patch
   }
 }
 
@@ -228,7 +243,7 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 // XOR 2 on pixels with bit 3 set: conflict-free fragment reads), so each fragment is three
 // ds_read_b128 and the split is done once per value instead of once per wave and tap that
 // reads it (the per-wave gather-and-split cost 0.12 of 0.20 ms, r03zb; now 0.17 ms).
-// Patches run two units ahead of the MFMAs (waves 0-3 load them into registers and store them
+// Patches run two units ahead of the MFMAs (all 8 waves load them into registers and store them
 // into two patch buffers); one barrier per unit.  The output leaves in one burst per unit after
 // the MFMAs: streaming it out under them (one store per MFMA group, or two 4-wave blocks per CU
 // drifting apart, or waves 4-7 storing a phase late) measured slower (r03zf-r03zj).
@@ -249,7 +264,6 @@ __global__ void __launch_bounds__(512, 1)
   const int li = lane & 15, lq = lane >> 4;
   const int nbase = (w & 3) * (COUT / 4);
   const int mt0 = 2 * (w >> 2);
-  const bool stager = w < 4;  // waves 0-3 carry the patch pipeline
   const int S = (g.TC + 31) / 32;
   const int PSZ = g.C * g.k * g.PW;
   const int zero_off = PSZ;
@@ -299,21 +313,19 @@ __global__ void __launch_bounds__(512, 1)
     }
   };
 
-  EdgePatchMap pm;
-  edge_patch_map(g, pm, tid & 255);
-  const long long u0 = blockIdx.x, gs = gridDim.x;
-  float pr[PREG];
+  // all 512 threads stage patches, unconditionally: units past the end load the last one (into a
+  // buffer nothing reads)
+  EdgePatchMapT<512> pm;
+  edge_patch_map(g, pm, tid);
+  const long long u0 = blockIdx.x, gs = gridDim.x, ulast = g.units - 1;
+  float pr[EdgePatchMapT<512>::R];
   // prologue: patch(u0) -> buffer 0, planes(u0) -> plane buffer 0, patch(u0 + gs) -> buffer 1
-  if (u0 < g.units && stager) {
-    edge_patch_load(g, pm, u0, pr);
-    edge_patch_store(g, pr, lds, tid);
-  }
+  edge_patch_load(g, pm, u0, pr);
+  edge_patch_store<512>(g, pr, lds, tid);
   __syncthreads();
-  if (u0 < g.units) build(lds, bpl);
-  if (u0 + gs < g.units && stager) {
-    edge_patch_load(g, pm, u0 + gs, pr);
-    edge_patch_store(g, pr, lds + bufsz, tid);
-  }
+  build(lds, bpl);
+  edge_patch_load(g, pm, min(u0 + gs, ulast), pr);
+  edge_patch_store<512>(g, pr, lds + bufsz, tid);
   floatx4v ob[2][NTW];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -329,8 +341,8 @@ __global__ void __launch_bounds__(512, 1)
     // buffer it & 1 (the previous iteration's) is done
     __syncthreads();
     const long long u1 = u + gs, u2 = u + 2 * gs;
-    if (u2 < g.units && stager) edge_patch_load(g, pm, u2, pr);
-    if (u1 < g.units) build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);
+    edge_patch_load(g, pm, min(u2, ulast), pr);
+    build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);
     const __bf16* planes = bpl + (it & 1) * 3 * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
@@ -359,7 +371,7 @@ __global__ void __launch_bounds__(512, 1)
     }
     // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration),
     // before this unit's global stores: waiting for its loads then never waits for them
-    if (u2 < g.units && stager) edge_patch_store(g, pr, lds + (it & 1) * bufsz, tid);
+    edge_patch_store<512>(g, pr, lds + (it & 1) * bufsz, tid);
     // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li).  The stored values
     // stay in registers of their own (`ob`, live across the unit loop): overwriting a store's data
     // registers waits for the store
@@ -601,6 +613,8 @@ bool edge_geom(EdgeGeom& g, const float* x, long long sn, long long sc, long lon
   g.TC = k * k * C;
   g.units_per_row = (Wo + SEG - 1) / SEG;
   g.units = (long long)N * Ho * g.units_per_row;
+  // 32-bit unit indices and in-image offsets (edge_patch_load)
+  if (g.units >= (1LL << 31) || (long long)(C - 1) * sc + (long long)(H - 1) * sh + W >= (1LL << 31)) return false;
   return g.C * g.k * g.PW <= PMAX;
 }
 
