@@ -121,6 +121,8 @@ SIGNATURES = {
     "ic_philox_advance": (c_int, [c_void, c_ull, c_void]),
     "ic_philox_kat": (c_int, [c_void, c_void, c_int, c_void]),
     "ic_psnr": (c_int, [c_void, c_void, c_int, c_ll, c_float, c_void, c_void]),
+    "ic_psnr_ws": (c_size, [c_int, c_ll]),
+    "ic_psnr_ex": (c_int, [c_void, c_void, c_int, c_ll, c_float, c_void, c_void, c_size, c_void]),
     "ic_images_u8_to_input": (c_int, [c_void, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void, c_void, c_void,
                                       c_void]),
     "ic_adamw_step": (c_int, [P(ICAdamWTensor), c_int, ctypes.c_double, ctypes.c_double, c_float, c_float, c_ll,

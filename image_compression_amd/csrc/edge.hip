@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(512, 1)
     EC3_T(0);
     __syncthreads();
     EC3_T(1);
-    const long long u1 = u + gs, u2 = u + 2 * gs;
+    const long long u2 = u + 2 * gs;
     edge_patch_load(g, pm, min(u2, ulast), pr);
     EC3_T(2);
     build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);

@@ -11,7 +11,8 @@ Kodak evaluator and its metrics, on HIP kernels.
   BatchAverageMeter (per-image mean) for metrics.
 * `Evaluator.run_eval(batches)` — engine/evaluator.py:67-105: eval mode,
   no_grad, forward, drop total_loss, update metrics and losses; returns the
-  mean results dict {psnr, ms_ssim, bpp, y_entropy, z_entropy, <distortion>}.
+  mean results dict {psnr, ms_ssim, bpp, y_entropy, z_entropy, <distortion>};
+  `graph=True` replays a hipGraph-captured forward per input shape (`GraphForward`).
 """
 import ctypes
 
@@ -29,9 +30,13 @@ def psnr(a, b, max_val=255.0):
     if a.shape != b.shape:
         raise RuntimeError(f"psnr: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
     N = a.shape[0]
+    L = _lib.load()
+    per = a.numel() // N
     out = torch.empty(N, device=a.device, dtype=torch.float32)
-    _lib.check(_lib.load().ic_psnr(_lib.ptr(a), _lib.ptr(b), N, ctypes.c_longlong(a.numel() // N), float(max_val),
-                                   _lib.ptr(out), _lib.stream_of(a)), "psnr")
+    nb = L.ic_psnr_ws(N, per)
+    buf = _lib.workspace(nb, a.device)
+    _lib.check(L.ic_psnr_ex(_lib.ptr(a), _lib.ptr(b), N, per, float(max_val), _lib.ptr(out), _lib.ptr(buf), nb,
+                            _lib.stream_of(a)), "psnr")
     return out
 
 
@@ -115,14 +120,63 @@ class Monitor:
         return self.results
 
 
+class GraphForward:
+    """The eval-mode forward (model.eval(): rounding instead of noise) captured once into a
+    hipGraph for one input shape and replayed per batch: the reference's Kodak evaluator runs
+    batch-1 512x768 forwards (engine/evaluator.py:87-105), ~100 launches each, many of them on
+    the 8x12..32x48 hyperprior maps where a launch costs more than its work.  `x_tilde` and
+    `losses` are the graph's static outputs, overwritten by the next call.  The hyperprior side
+    stream joins the capture (it forks from and rejoins the capture stream)."""
+
+    def __init__(self, model, example_x, warmup=2):
+        if not example_x.is_cuda:
+            raise RuntimeError("GraphForward needs a ROCm device tensor")
+        self.model = model
+        self.x = example_x.detach().clone()
+        dev = self.x.device
+        was_training = model.training
+        model.eval()
+        try:
+            with torch.no_grad():
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    for _ in range(warmup):  # allocator pools warm, kernels loaded
+                        model(self.x)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self.x_tilde, self.losses = model(self.x)
+        finally:
+            model.train(was_training)
+
+    def __call__(self, x):
+        self.x.copy_(x)
+        self.graph.replay()
+        return self.x_tilde, self.losses
+
+
 class Evaluator:
     """engine/evaluator.py:44-123 without the data loader / file outputs:
-    run_eval(batches) over an iterable of [N,3,H,W] images in [0,1]."""
+    run_eval(batches) over an iterable of [N,3,H,W] images in [0,1].  graph=True replays one
+    captured forward per input shape (GraphForward) instead of launching it eagerly."""
 
-    def __init__(self, model, device=None):
+    def __init__(self, model, device=None, graph=False):
         self.model = model
         self.device = device
         self.monitor = Monitor(model.loss_names)
+        self.graph = graph
+        self._graphs = {}
+
+    def _forward(self, imgs):
+        if not (self.graph and imgs.is_cuda):
+            return self.model(imgs)
+        key = (tuple(imgs.shape), imgs.device)
+        g = self._graphs.get(key)
+        if g is None:
+            g = self._graphs[key] = GraphForward(self.model, imgs)
+        x_tilde, losses = g(imgs)
+        return x_tilde, dict(losses)
 
     @torch.no_grad()
     def run_eval(self, batches):
@@ -133,7 +187,7 @@ class Evaluator:
             for imgs in batches:
                 if self.device is not None:
                     imgs = imgs.to(self.device, non_blocking=True)
-                x_tilde, losses = self.model(imgs)
+                x_tilde, losses = self._forward(imgs)
                 losses.pop("total_loss")
                 self.monitor.update_metric(x_tilde, imgs)
                 self.monitor.update_loss(**losses)

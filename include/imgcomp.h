@@ -367,6 +367,11 @@ int ic_msssim_bwd(int N, int C, int H, int W, int nlev, int filter_size, float f
 /* ---- evaluation metric: per-image PSNR in dB (utils/metric.py:26-36) of images scaled by
  *      max_val: out[n] = 10 (2 log10(max_val) - log(mse_n) / ln 10), a, b [N][per_image] ---- */
 int ic_psnr(const float* a, const float* b, int N, long long per_image, float max_val, float* out, void* stream);
+/* the same over 128 blocks per image: partials in ws (ic_psnr_ws bytes), summed in fixed order
+ * (deterministic); N <= 65535 */
+size_t ic_psnr_ws(int N, long long per_image);
+int ic_psnr_ex(const float* a, const float* b, int N, long long per_image, float max_val, float* out, void* ws,
+               size_t ws_bytes, void* stream);
 
 /* ---- host data path: uint8 HWC images (byte strides sn, sh, sw; channel stride 1) -> fp32
  *      NCHW model input (x/255 - mean[c]) / std[c] (transforms.py ToTensor, ChannelFirst,
