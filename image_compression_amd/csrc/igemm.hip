@@ -740,13 +740,15 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 }
 
 // ------------------------------------------------------------------ split, every operand by LDS-DMA
-// The split implicit GEMM on 256 x 192 tiles, eight waves of 64 x 96, one block per CU, with
+// The split implicit GEMM on 256 x 192 tiles, eight waves of 32 x 192, one block per CU, with
 // no register staging: per K chunk (32 channels of one tap) the block's 256 gathered fp32
 // activation rows (32 KB) and the three pre-split weight planes (36 KB) arrive by LDS-DMA
 // (global_load_lds_dwordx4 from inline asm, so the compiler does not wait for the DMA before
 // LDS reads) into one of two stages; one barrier per chunk publishes chunk c and frees the
 // stage that chunk c + 1's DMA, issued right after it, overwrites.  Each wave splits its own A
-// fragments into three bf16 terms after reading them (8 fp32 per lane per 16-row tile) and runs
+// fragments into three bf16 terms after reading them (8 fp32 per lane per 16-row tile) — the 32
+// rows it DMAs, each split by one wave (64 x 96 wave tiles split every row in two waves: 2.6 %
+// slower on the big layers, 1.4 % per C2 step, r03zw) — and runs
 // ig_kernel_x3s's six products per (i, j) in the same order over the same chunk order, so the
 // result is bitwise that kernel's.  Per chunk a 256-row tile stages the weights once for twice
 // the rows of ig_kernel_x3s<128, ...> (68 vs 104 KB per 256 rows), and no VALU or ds_write
@@ -755,6 +757,9 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 // (ig_swa): the four 16-lane groups of a ds_read_b128 fragment read hit distinct bank slots.
 #ifndef IG_X3D
 #define IG_X3D 1
+#endif
+#ifndef IG_X3D_WM
+#define IG_X3D_WM 32  // rows per wave: 32 x 192 wave tiles (64: 64 x 96, each A row split by two waves)
 #endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
@@ -777,7 +782,7 @@ __device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
 __device__ __forceinline__ int ig_swa(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
 
 __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
-  constexpr int BM = 256, BN = 192, WM = 64, WN = 96, TM = WM / 16, TN = WN / 16, LDB = 32;
+  constexpr int BM = 256, BN = 192, WM = IG_X3D_WM, WN = BM * BN / 8 / WM, TM = WM / 16, TN = WN / 16, LDB = 32;
   constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
   constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
   constexpr int STAGE = ASTAGE + BSTAGE;
@@ -853,7 +858,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     }
   };
 
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / (BN / WN), wn = w % (BN / WN);
   const int r = lane & 15, g = lane >> 4;
   const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
   const int bch = 8 * (g ^ ig_swz(r));
