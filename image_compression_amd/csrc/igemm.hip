@@ -761,6 +761,12 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D_WM
 #define IG_X3D_WM 32  // rows per wave: 32 x 192 wave tiles (64: 64 x 96, each A row split by two waves)
 #endif
+#ifndef IG_X3D_DMA_AT
+#define IG_X3D_DMA_AT 2  // where the next chunk's DMA issues: 0 after the A split, 1 before it, 2 among the MFMAs
+#endif
+#ifndef IG_X3D_DMA_J
+X
+#endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
 #endif
@@ -878,6 +884,10 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     __syncthreads();
     const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
     const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
+    if (IG_X3D_DMA_AT == 1 && c + 1 < ce) {
+      issue(cn, tn, (c + 1 - cb) & 1);
+      if (++tn == T) { tn = 0; ++cn; }
+    }
     bf16x8 a[3][TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -892,12 +902,16 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
     }
     // the next chunk's DMA, between the split (VALU) and the MFMAs (r03p: 1 % faster than before the split)
-    if (c + 1 < ce) {
+    if (IG_X3D_DMA_AT == 0 && c + 1 < ce) {
       issue(cn, tn, (c + 1 - cb) & 1);
       if (++tn == T) { tn = 0; ++cn; }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      if (IG_X3D_DMA_AT == 2 && j == IG_X3D_DMA_J && c + 1 < ce) {
+        issue(cn, tn, (c + 1 - cb) & 1);
+        if (++tn == T) { tn = 0; ++cn; }
+      }
       bf16x8 b[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 16 + r) * LDB + bch);
