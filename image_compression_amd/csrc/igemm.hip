@@ -765,7 +765,7 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #define IG_X3D_DMA_AT 2  // where the next chunk's DMA issues: 0 after the A split, 1 before it, 2 among the MFMAs
 #endif
 #ifndef IG_X3D_DMA_J
-X
+#define IG_X3D_DMA_J 4  // DMA_AT 2: before n-tile j's MFMAs (r03zx-r03zy: j = 4 of 12, 1.7-2.7 % per C2 step over 0)
 #endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
