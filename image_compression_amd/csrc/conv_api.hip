@@ -55,8 +55,10 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
     float* wp = (float*)ws;
     int ky[IC_MAXT], kx[IC_MAXT];
     for (int t = 0; t < T; ++t) { ky[t] = t / k; kx[t] = t % k; }
-    int rc = pack_weights(W, y->c, x->c, k, 0, 1, T, ky, kx, Npad, Kp, wp, s);
-    if (rc) return rc;
+    if (!(math & IC_MATH_WPACKED)) {
+      int rc = pack_weights(W, y->c, x->c, k, 0, 1, T, ky, kx, Npad, Kp, wp, s);
+      if (rc) return rc;
+    }
     return edge_conv_run(x->data, x->sn, x->sc, x->sh, x->sw, x->n, x->c, x->h, x->w, wp, Kp, bias, k, stride, pad,
                          y->data, y->sn, y->sc, y->sh, y->sw, y->c, y->h, y->w, epi == EPI_RELU, s, split);
   }
@@ -194,8 +196,10 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   float* wp = cv.take(wpb);
   d.partial = part ? cv.take(part) : nullptr;
   P.wp = wp;
-  int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.x3 ? 2 : d.bf16);
-  if (rc) return rc;
+  if (!(math & IC_MATH_WPACKED)) {
+    int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.x3 ? 2 : d.bf16);
+    if (rc) return rc;
+  }
   return ig_run(d, s);
 }
 
@@ -282,8 +286,10 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
       for (int t = 0; t < d.ph[p].T; ++t) { aky[t0 + t] = pky[p][t]; akx[t0 + t] = pkx[p][t]; }
       t0 += d.ph[p].T;
     }
-    int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)base, s, 2);
-    if (rc) return rc;
+    if (!(math & IC_MATH_WPACKED)) {
+      int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)base, s, 2);
+      if (rc) return rc;
+    }
     return ig_run(d, s);
   }
   size_t wpb[IC_MAXPH];
@@ -312,13 +318,16 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
       for (int t = 0; t < d.ph[p].T; ++t) { aky[t0 + t] = pky[p][t]; akx[t0 + t] = pkx[p][t]; }
       t0 += d.ph[p].T;
     }
-    int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)d.ph[0].wp, s, d.bf16);
-    if (rc) return rc;
+    if (!(math & IC_MATH_WPACKED)) {
+      int rc = pack_weights(W, x->c, y->c, k, 1, 0, ttot, aky, akx, d.Npad, d.Kc, (float*)d.ph[0].wp, s, d.bf16);
+      if (rc) return rc;
+    }
     return ig_run(d, s);
   }
   for (int p = 0; p < np; ++p) {
     float* wp = cv.take(wpb[p]);
     d.ph[p].wp = wp;
+    if (math & IC_MATH_WPACKED) continue;
     int rc = pack_weights(W, x->c, y->c, k, 1, d.generic, d.ph[p].T, pky[p], pkx[p], d.Npad, d.Kc, wp, s, d.bf16);
     if (rc) return rc;
   }

@@ -81,6 +81,60 @@ Tensor conv2d_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
   return y;
 }
 
+// The forward with a caller-owned workspace that persists across calls (eval-mode weight caching,
+// functional._cached_fwd): grown here when too small (only on a packing call — with IC_MATH_WPACKED the
+// pack must already be in it, so a short workspace is an error).
+void ensure_ws(Tensor& ws, size_t nb, int64_t math, const char* what) {
+  if ((size_t)ws.numel() >= nb) return;
+  TORCH_CHECK(!(math & IC_MATH_WPACKED), "imgcomp: ", what, ": IC_MATH_WPACKED with a workspace of ", ws.numel(),
+              " bytes, the op needs ", nb);
+  ws.resize_({(int64_t)nb});
+}
+Tensor conv2d_fwd_ws(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b, int64_t stride, int64_t pad,
+                     int64_t act, int64_t math, Tensor& ws) {
+  check_operand(x, "x");
+  check_operand(w, "weight");
+  if (b.has_value()) check_operand(*b, "bias");
+  TORCH_CHECK(ws.device() == x.device() && ws.scalar_type() == at::kByte && ws.dim() == 1 && ws.is_contiguous(),
+              "conv2d_fwd_ws: the workspace must be a contiguous uint8 vector on the input's device");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == w.size(3), "conv2d: weight ", w.sizes(),
+              " does not match input ", x.sizes());
+  const int64_t k = w.size(2);
+  const int64_t ho = (x.size(2) + 2 * pad - k) / stride + 1, wo = (x.size(3) + 2 * pad - k) / stride + 1;
+  Tensor y = new_act(x, x.size(0), w.size(0), ho, wo);
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb = ic_conv2d_fwd_ws_ex(&ax, (int)k, (int)stride, (int)pad, &ay, (int)(math & ~IC_MATH_WPACKED));
+  ensure_ws(ws, nb, math, "conv2d_fwd_ws");
+  check_rc(ic_conv2d_fwd_ex(&ax, w.data_ptr<float>(), opt_ptr(b), (int)k, (int)stride, (int)pad, &ay, (int)act,
+                            (int)math, ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+           "conv2d_fwd_ws");
+  return y;
+}
+Tensor conv_transpose2d_fwd_ws(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b, int64_t stride,
+                               int64_t pad, int64_t output_padding, int64_t act, int64_t math, Tensor& ws) {
+  check_operand(x, "x");
+  check_operand(w, "weight");
+  if (b.has_value()) check_operand(*b, "bias");
+  TORCH_CHECK(ws.device() == x.device() && ws.scalar_type() == at::kByte && ws.dim() == 1 && ws.is_contiguous(),
+              "conv_transpose2d_fwd_ws: the workspace must be a contiguous uint8 vector on the input's device");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == x.size(1) && w.size(2) == w.size(3), "conv_transpose2d: weight ",
+              w.sizes(), " does not match input ", x.sizes());
+  const int64_t k = w.size(2);
+  const int64_t ho = (x.size(2) - 1) * stride - 2 * pad + k + output_padding;
+  const int64_t wo = (x.size(3) - 1) * stride - 2 * pad + k + output_padding;
+  Tensor y = new_act(x, x.size(0), w.size(1), ho, wo);
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb =
+      ic_conv_transpose2d_fwd_ws_ex(&ax, (int)k, (int)stride, (int)pad, &ay, (int)(math & ~IC_MATH_WPACKED));
+  ensure_ws(ws, nb, math, "conv_transpose2d_fwd_ws");
+  check_rc(ic_conv_transpose2d_fwd_ex(&ax, w.data_ptr<float>(), opt_ptr(b), (int)k, (int)stride, (int)pad, &ay,
+                                      (int)act, (int)math, ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+           "conv_transpose2d_fwd_ws");
+  return y;
+}
+
 // dx has the shape and memory format of x
 Tensor conv2d_dgrad(const Tensor& dy, const Tensor& w, const Tensor& x, int64_t stride, int64_t pad, int64_t math) {
   check_operand(dy, "dy");
@@ -662,6 +716,10 @@ Tensor conv2d_fwd_meta(const Tensor& x, const Tensor& w, const c10::optional<Ten
   return at::empty({x.size(0), w.size(0), (x.size(2) + 2 * pad - k) / stride + 1, (x.size(3) + 2 * pad - k) / stride + 1},
                    x.options().memory_format(act_format(w.size(0))));
 }
+Tensor conv2d_fwd_ws_meta(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b, int64_t stride,
+                          int64_t pad, int64_t act, int64_t math, Tensor&) {
+  return conv2d_fwd_meta(x, w, b, stride, pad, act, math);
+}
 Tensor conv2d_dgrad_meta(const Tensor& dy, const Tensor&, const Tensor& x, int64_t, int64_t, int64_t) {
   return at::empty(x.sizes(), dy.options().memory_format(x.suggest_memory_format()));
 }
@@ -675,6 +733,10 @@ Tensor conv_transpose2d_fwd_meta(const Tensor& x, const Tensor& w, const c10::op
   return at::empty({x.size(0), w.size(1), (x.size(2) - 1) * stride - 2 * pad + k + op,
                     (x.size(3) - 1) * stride - 2 * pad + k + op},
                    x.options().memory_format(act_format(w.size(1))));
+}
+Tensor conv_transpose2d_fwd_ws_meta(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b,
+                                    int64_t stride, int64_t pad, int64_t op, int64_t act, int64_t math, Tensor&) {
+  return conv_transpose2d_fwd_meta(x, w, b, stride, pad, op, act, math);
 }
 Tensor conv_transpose2d_dgrad_meta(const Tensor& dy, const Tensor&, const Tensor& x, int64_t, int64_t, int64_t) {
   return at::empty(x.sizes(), dy.options().memory_format(act_format(x.size(1))));
@@ -770,11 +832,15 @@ std::tuple<Tensor, Tensor> msssim_bwd_meta(const Tensor& g, const Tensor&, at::I
 
 TORCH_LIBRARY(imgcomp, m) {
   m.def("conv2d_fwd(Tensor x, Tensor weight, Tensor? bias, int stride, int padding, int act, int math) -> Tensor");
+  m.def("conv2d_fwd_ws(Tensor x, Tensor weight, Tensor? bias, int stride, int padding, int act, int math, "
+        "Tensor(a!) ws) -> Tensor");
   m.def("conv2d_dgrad(Tensor dy, Tensor weight, Tensor x, int stride, int padding, int math) -> Tensor");
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor weight, int stride, int padding, bool bias, int math) -> "
         "(Tensor, Tensor)");
   m.def("conv_transpose2d_fwd(Tensor x, Tensor weight, Tensor? bias, int stride, int padding, int output_padding, "
         "int act, int math) -> Tensor");
+  m.def("conv_transpose2d_fwd_ws(Tensor x, Tensor weight, Tensor? bias, int stride, int padding, "
+        "int output_padding, int act, int math, Tensor(a!) ws) -> Tensor");
   m.def("conv_transpose2d_dgrad(Tensor dy, Tensor weight, Tensor x, int stride, int padding, int math) -> Tensor");
   m.def("conv_transpose2d_wgrad(Tensor x, Tensor dy, Tensor weight, int stride, int padding, bool bias, int math) -> "
         "(Tensor, Tensor)");
@@ -820,6 +886,8 @@ TORCH_LIBRARY(imgcomp, m) {
 
 TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm's HIP device key
   m.impl("conv2d_fwd", conv2d_fwd);
+  m.impl("conv2d_fwd_ws", conv2d_fwd_ws);
+  m.impl("conv_transpose2d_fwd_ws", conv_transpose2d_fwd_ws);
   m.impl("conv2d_dgrad", conv2d_dgrad);
   m.impl("conv2d_wgrad", conv2d_wgrad);
   m.impl("conv_transpose2d_fwd", conv_transpose2d_fwd);
@@ -858,6 +926,8 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
 
 TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("conv2d_fwd", conv2d_fwd_meta);
+  m.impl("conv2d_fwd_ws", conv2d_fwd_ws_meta);
+  m.impl("conv_transpose2d_fwd_ws", conv_transpose2d_fwd_ws_meta);
   m.impl("conv2d_dgrad", conv2d_dgrad_meta);
   m.impl("conv2d_wgrad", conv2d_wgrad_meta);
   m.impl("conv_transpose2d_fwd", conv_transpose2d_fwd_meta);

@@ -7,7 +7,7 @@ and the divide fused in the epilogue (csrc/gdn.hip)."""
 import torch
 import torch.nn as nn
 
-from ...functional import GDNFn, NonNegFn, ReLUFn
+from ...functional import GDNFn, NonNegFn, ReLUFn, nonneg_cached
 
 
 class NonNegativeParam(nn.Module):
@@ -22,7 +22,7 @@ class NonNegativeParam(nn.Module):
         self.param = nn.Parameter(torch.sqrt(torch.max(init_val + ped, ped)))
 
     def forward(self):
-        return NonNegFn.apply(self.param, float(self.bound), float(self.pedestal))
+        return nonneg_cached(self.param, float(self.bound), float(self.pedestal))
 
 
 class GDN(nn.Module):

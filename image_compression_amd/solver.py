@@ -44,7 +44,7 @@ class AdamW(torch.optim.Optimizer):
                 loss = closure()
         # one launch per (betas, eps, step) family; the reference builds all
         # groups with the same betas / eps, and every parameter steps together
-        fams = {}
+        fams, stepped = {}, []
         for group in self.param_groups:
             for p in group["params"]:
                 if p.grad is None:
@@ -58,6 +58,7 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
+                stepped.append(p)
                 key = (p.device, tuple(group["betas"]), group["eps"], int(st["step"].item()))
                 fams.setdefault(key, []).append(
                     _lib.ICAdamWTensor(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
@@ -69,6 +70,10 @@ class AdamW(torch.optim.Optimizer):
                                                  self.clip_value, step,
                                                  _lib.c_void(torch.cuda.current_stream(dev).cuda_stream)),
                        "adamw_step")
+        # the kernel writes the parameters behind autograd's back: bump their version counters as
+        # an in-place torch op would (saved-tensor checks, functional.weight_cache)
+        if stepped:
+            torch.autograd.graph.increment_version(stepped)
         return loss
 
 

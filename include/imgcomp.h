@@ -95,6 +95,13 @@ int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stri
  *      3/8 of the native fp32 MFMA's cycles per MAC); layers with reduction channels % 32 == 0
  *      and >= 64 output channels, others run the native fp32 kernel. */
 #define IC_MATH_SPLIT 2
+/*      IC_MATH_WPACKED (conv / transposed-conv forward only, or-ed into a math mode): the workspace
+ *      already holds this weight's pack, written by an earlier forward with the same weight
+ *      values, activation shapes / strides, math mode and workspace; the pack launch is skipped
+ *      (eval-mode weight caching, functional.py).  Paths whose pack is not kept in the workspace
+ *      (the im2col fallback, the row-stationary transposed edge) ignore it.  The caller owns the invalidation: any change of
+ *      the weight needs a forward without the flag first. */
+#define IC_MATH_WPACKED 4
 size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
 int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
                      const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);

@@ -268,6 +268,11 @@ def _meta_cases():
         "msssim_bwd": (lambda o: o.msssim_bwd(_meta(()), _meta(1000), [2, 3, 256, 256], 5, 11, 1.5, 255.0, True, 0,
                                               0.01, 0.03, 1e-5, w, True, False), [(2, 3, 256, 256), (0,)]),
         "conv2d_fwd": (lambda o: o.conv2d_fwd(x, _meta(192, 192, 5, 5), None, 2, 2, 0, 2), [(2, 192, 8, 8)]),
+        "conv2d_fwd_ws": (lambda o: o.conv2d_fwd_ws(x, _meta(192, 192, 5, 5), None, 2, 2, 0, 2,
+                                                    _meta(16, dtype=torch.uint8)), [(2, 192, 8, 8)]),
+        "conv_transpose2d_fwd_ws": (lambda o: o.conv_transpose2d_fwd_ws(_meta(2, 192, 8, 8, cl=True),
+                                                                        _meta(192, 192, 5, 5), None, 2, 2, 1, 0, 2,
+                                                                        _meta(16, dtype=torch.uint8)), [s]),
         "conv2d_dgrad": (lambda o: o.conv2d_dgrad(_meta(2, 192, 8, 8, cl=True), _meta(192, 192, 5, 5), x, 2, 2, 2),
                          [s]),
         "conv2d_wgrad": (lambda o: o.conv2d_wgrad(x, _meta(2, 192, 8, 8, cl=True), _meta(192, 192, 5, 5), 2, 2, True,

@@ -89,3 +89,59 @@ def test_graph_forward_matches_eager_and_evaluator():
     res = Evaluator(model).run_eval(imgs)
     resg = Evaluator(model, graph=True).run_eval(imgs)
     assert res == resg, (res, resg)
+
+
+def test_weight_cache_is_bitwise_and_invalidates():
+    """functional.weight_cache (Evaluator.run_eval's eager path): forwards that reuse the weight
+    packs (IC_MATH_WPACKED) and GDN re-parameterisations equal uncached forwards bitwise, on both
+    image orientations; an in-place weight change and an AdamW step (which bumps the parameters'
+    version counters after its kernel) invalidate the entries; the table empties on scope exit."""
+    from image_compression_amd import functional as F
+    from image_compression_amd import get_cfg_defaults, modelling
+    from image_compression_amd.solver import AdamW
+    cfg = get_cfg_defaults()
+    cfg.MODEL.LOSS.REDUCTION = "mean"
+    cfg.MODEL.LOSS.DISTORTION_LOSS_WEIGHT = 256.0
+    torch.manual_seed(0)
+    model = modelling.build_model(cfg).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    imgs = [torch.rand(1, 3, 256, 384, device=DEV, generator=g), torch.rand(1, 3, 384, 256, device=DEV, generator=g)]
+
+    def run():
+        with torch.no_grad():
+            return [model(im) for im in imgs]
+
+    def same(a, b):
+        for (xa, la), (xb, lb) in zip(a, b):
+            assert torch.equal(xa, xb)
+            for k in la:
+                assert torch.equal(la[k], lb[k]), k
+
+    model.eval()
+    ref = run()
+    with F.weight_cache():
+        same(run(), ref)          # fills the cache (packs)
+        assert len(F._WCACHE) > 0
+        same(run(), ref)          # reuses it (no packs)
+        same(run(), ref)
+        w = model.analysis_transform.layers[2].weight
+        with torch.no_grad():
+            w.mul_(1.01)          # in-place change: version bump -> re-pack
+        F_ = run()
+    ref2 = run()
+    same(F_, ref2)
+    assert len(F._WCACHE) == 0
+    assert not torch.equal(ref2[0][0], ref[0][0])
+    # an AdamW step writes the parameters from its kernel and bumps their versions
+    model.train()
+    opt = AdamW(model.parameters(), lr=1e-3)
+    x, losses = model(imgs[0])
+    losses["total_loss"].backward()
+    v0 = w._version
+    opt.step()
+    assert w._version > v0
+    model.eval()
+    ref3 = run()
+    with F.weight_cache():
+        same(run(), ref3)
+        same(run(), ref3)

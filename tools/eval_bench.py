@@ -2,7 +2,8 @@
 """Eval-path (inference) throughput: the reference's Kodak evaluator workload
 (engine/evaluator.py:87-105 — model.eval(), batch-1 512x768 forwards, then bpp / PSNR /
 MS-SSIM), on synthetic images resident in HBM with random-init weights (Kodak and trained
-checkpoints are not in the container).  Times, per image: the eager forward, the hipGraph
+checkpoints are not in the container).  Times, per image: the eager forward (without and with
+functional.weight_cache), the hipGraph
 replay (evaluation.GraphForward), and the whole Evaluator.run_eval with and without the graph
 (metrics included, host sync per image as the reference's monitor does).  One JSON line.
 
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--width", type=int, default=768)
     args = ap.parse_args()
     from image_compression_amd import get_cfg_defaults, modelling
+    from image_compression_amd import functional as F
     from image_compression_amd.evaluation import Evaluator, GraphForward
     cfg = get_cfg_defaults()
     cfg.MODEL.LOSS.REDUCTION = "mean"
@@ -53,6 +55,11 @@ def main():
         for im in imgs[:2]:
             model(im)
         t_eager = timed(lambda: [model(im) for im in imgs])
+        with F.weight_cache():  # weight packs / GDN re-parameterisations kept across images
+            t_cached = timed(lambda: [model(im) for im in imgs])
+            xc, lc = model(imgs[0])
+        xe0, le0 = model(imgs[0])
+        same_cached = bool(torch.equal(xe0, xc)) and all(torch.equal(le0[k], lc[k]) for k in le0)
         gf = GraphForward(model, imgs[0])
         t_graph = timed(lambda: [gf(im) for im in imgs])
         xe, le = model(imgs[0])
@@ -67,12 +74,15 @@ def main():
         "metric": f"eval forward images/s ({args.height}x{args.width}, batch {args.batch})",
         "unit": "images/s",
         "eager_forward": round(n / t_eager, 2),
+        "eager_forward_weight_cache": round(n / t_cached, 2),
         "graph_forward": round(n / t_graph, 2),
         "evaluator_eager": round(n / t_ev, 2),
         "evaluator_graph": round(n / t_evg, 2),
-        "ms_per_image": {"eager": round(1e3 * t_eager / n, 3), "graph": round(1e3 * t_graph / n, 3),
+        "ms_per_image": {"eager": round(1e3 * t_eager / n, 3), "eager_weight_cache": round(1e3 * t_cached / n, 3),
+                         "graph": round(1e3 * t_graph / n, 3),
                          "evaluator_eager": round(1e3 * t_ev / n, 3), "evaluator_graph": round(1e3 * t_evg / n, 3)},
         "graph_bitwise_equal_eager": same,
+        "weight_cache_bitwise_equal_eager": same_cached,
         "images": n,
         "compute_dtype": cfg.MODEL.COMPUTE_DTYPE,
         "data": "synthetic uniform [0,1) images resident in HBM; random-init weights (reference init, seed 0)",
