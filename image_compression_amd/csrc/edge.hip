@@ -786,6 +786,10 @@ __global__ void __launch_bounds__(64 * NWV, 2)
 #define TF2_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) on the input-row kernel
 #endif
 constexpr int TF2_RS = 8;  // ring slots: rows 2r - pad - 2 .. 2r - pad + k - 1 in flight
+constexpr int TF2_HALO = 2;  // input columns loaded left of a column segment (k <= 5, pad >= 0)
+// input columns a segment owns when the row is wider than the block (WMAX = 128): its output
+// columns need input columns up to (2 (sg + 1) wseg - 1 + pad) / 2 <= base + WMAX - 1 for pad <= 5
+constexpr int TF2_WSEG = 120;
 
 // X3 (IC_MATH_SPLIT, Cin % 32 == 0): fp32 by the exact three-term bf16 split
 // on v_mfma_f32_16x16x32_bf16 (six products per MAC, 3/8 of the fp32 MFMA's
@@ -797,7 +801,8 @@ template <int NWV, bool X3>
 __global__ void __launch_bounds__(64 * NWV, 1)
     tconv_few2_kernel(const float* __restrict__ x, int N, int Hin, int Win, int Cin, const float* __restrict__ W,
                       int Cout, int k, int pad, const float* __restrict__ bias, int relu, float* __restrict__ y,
-                      long long ysn, long long ysc, long long ysh, long long ysw, int Hout, int Wout, int run) {
+                      long long ysn, long long ysc, long long ysh, long long ysw, int Hout, int Wout, int run,
+                      int wseg) {
   typedef __bf16 tb4 __attribute__((ext_vector_type(4)));
   typedef __bf16 tb8 __attribute__((ext_vector_type(8)));
   constexpr int WMAX = 16 * NWV;
@@ -844,20 +849,31 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   }
   __syncthreads();
 
+  // rows wider than WMAX run in column segments: segment sg owns input columns [sg wseg, (sg + 1) wseg)
+  // and output columns [2 sg wseg, 2 (sg + 1) wseg) (the last one: to Wout); it loads the WMAX
+  // input columns from sg wseg - TF2_HALO, which hold every input column its output columns take
+  // (2 ix = X + pad - kx, kx < k <= 5).  One segment (Win <= WMAX): base 0, all of Wout.
+  const int nseg = (Win + wseg - 1) / wseg;
+  const int sg = blockIdx.x % nseg;
+  const int bq = blockIdx.x / nseg;
+  const int base = nseg == 1 ? 0 : sg * wseg - TF2_HALO;
+  const int X0 = 2 * sg * wseg;
+  const int X1 = sg == nseg - 1 ? Wout : min(Wout, 2 * (sg + 1) * wseg);
   const int nrun = (Hin + run - 1) / run;
-  const int n = blockIdx.x / nrun;
-  const int r0 = (blockIdx.x - n * nrun) * run;
+  const int n = bq / nrun;
+  const int r0 = (bq - n * nrun) * run;
   const bool last = r0 + run >= Hin;
   const int rlast = last ? (Hout - 1 + pad) >> 1 : r0 + run - 1;   // last input row whose rows are emitted
   const int rfirst = r0 - (k - 1) / 2;
-  const int px = 16 * w + li;
+  const int px = 16 * w + li;  // this lane's column within the segment's WMAX
+  const int gx = base + px;    // ... and in the image
   const float* xn = x + (size_t)n * Hin * Win * Cin;
 
   floatx4v a0[12], a1[12];
   // fp32: a[u] = channels 16u + 4lq .. +3; X3: a[2s + h] = channels 32s + 8lq + 4h .. +3
   auto load = [&](int r, floatx4v (&a)[12]) {
-    const bool ok = r >= 0 && r < Hin && px < Win;
-    const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? px : 0)) * Cin + (X3 ? 8 : 4) * lq;
+    const bool ok = r >= 0 && r < Hin && gx >= 0 && gx < Win;
+    const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? gx : 0)) * Cin + (X3 ? 8 : 4) * lq;
 #pragma unroll
     for (int u = 0; u < 12; ++u) {
       const int off = X3 ? 32 * (u >> 1) + 4 * (u & 1) : 16 * u;
@@ -871,12 +887,12 @@ __global__ void __launch_bounds__(64 * NWV, 1)
       const int Y = 2 * r - pad + h;
       if (Y < 0 || Y >= Hout) continue;
       const float* sl = ring + (Y & (TF2_RS - 1)) * WMAX * 16;
-      for (int X = tid; X < Wout; X += NT) {
+      for (int X = X0 + tid; X < X1; X += NT) {
         float sum[4] = {0.f, 0.f, 0.f, 0.f};
         for (int kx = (X + pad) & 1; kx < k; kx += 2) {
           const int ix = (X + pad - kx) >> 1;
           if (ix < 0 || ix >= Win) continue;
-          const float* cp = sl + ix * 16 + kx * Cout;
+          const float* cp = sl + (ix - base) * 16 + kx * Cout;
           for (int o = 0; o < Cout; ++o) sum[o] += cp[o];
         }
         for (int o = 0; o < Cout; ++o) {
@@ -1080,15 +1096,18 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
 }
 
 int tconv_few_kind(int Hin, int Win, int k, int pad, int Hout) {
-  return (TCONV_FEW2 && Win <= 128 && k <= 5 && (Hout - 1 + pad) / 2 <= Hin + 2) ? IC_KERNEL_TCONV_FEW_ROWS
-                                                                                 : IC_KERNEL_TCONV_FEW;
+  // any width (column segments past 128), pad <= 5 (the segment halo)
+  return (TCONV_FEW2 && k <= 5 && pad <= 5 && (Hout - 1 + pad) / 2 <= Hin + 2 && Win <= 4096)
+             ? IC_KERNEL_TCONV_FEW_ROWS
+             : IC_KERNEL_TCONV_FEW;
 }
 
 // transposed conv 2x upsampling of a wide NHWC map to <= 4 channels (see tconv_few_kernel)
 bool tconv_few_ok(int Cin, int Cout, int k, int stride, int pad, long long xsc, long long xsw, long long xsh,
                   long long xsn, int Hin, int Win) {
   return stride == 2 && k <= 5 && k >= 1 && Cout >= 1 && Cout <= 4 && k * Cout <= 16 && Cin % 16 == 0 &&
-         Cin <= 192 && Win <= 256 && xsc == 1 && xsw == Cin && xsh == (long long)Win * Cin &&
+         Cin <= 192 && (Win <= 256 || (TCONV_FEW2 && pad <= 5 && Win <= 4096)) && xsc == 1 && xsw == Cin &&
+         xsh == (long long)Win * Cin &&
          xsn == (long long)Hin * Win * Cin && pad >= 0;
 }
 
@@ -1097,20 +1116,24 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
                   int Hout, int Wout, hipStream_t s, int split) {
   if (((uintptr_t)x & 15) || Hout < 1 || Wout < 1) return IC_ERR_ARG;
   if (tconv_few_kind(Hin, Win, k, pad, Hout) == IC_KERNEL_TCONV_FEW_ROWS) {
-    // input-row stationary: runs of input rows, about one block per CU
-    long long run = ((long long)N * Hin + 255) / 256;
+    // input-row stationary: runs of input rows (x column segments past 128), about one block per CU
+    const int wseg = Win <= 128 ? Win : TF2_WSEG;
+    const long long nseg = (Win + wseg - 1) / wseg;
+    long long run = ((long long)N * Hin * nseg + 255) / 256;
     if (run < 4) run = 4;
     if (run > Hin) run = Hin;
-    const long long blocks = (long long)N * ((Hin + run - 1) / run);
+    const long long blocks = (long long)N * ((Hin + run - 1) / run) * nseg;
+    if (blocks >= (1LL << 31)) return IC_ERR_ARG;
     if (TF2_SPLIT && split && Cin % 32 == 0)
       hipLaunchKernelGGL((tconv_few2_kernel<8, true>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W,
-                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
+                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run, wseg);
     else
       hipLaunchKernelGGL((tconv_few2_kernel<8, false>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W,
-                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run);
+                         Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run, wseg);
     IC_CHECK_LAUNCH();
     return IC_OK;
   }
+  if (Win > 256) return IC_ERR_ARG;  // the output-row kernels hold a row of <= 256 pixels
   const long long rows = (long long)N * ((Hout + 1) / 2);
   long long grid = 2 * (rows < 256 ? rows : 256);  // two parities, <= 2 blocks per CU
   if (Win <= 64)
