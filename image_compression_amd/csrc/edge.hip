@@ -786,6 +786,9 @@ __global__ void __launch_bounds__(64 * NWV, 2)
 #define TF2_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) on the input-row kernel
 #endif
 constexpr int TF2_RS = 8;  // ring slots: rows 2r - pad - 2 .. 2r - pad + k - 1 in flight
+#ifndef TF2_ABL
+#define TF2_ABL 0  // ablations (timing only): 1 no MFMAs, 2 no emission, 4 no input loads
+#endif
 constexpr int TF2_HALO = 2;  // input columns loaded left of a column segment (k <= 5, pad >= 0)
 // input columns a segment owns when the row is wider than the block (WMAX = 128): its output
 // columns need input columns up to (2 (sg + 1) wseg - 1 + pad) / 2 <= base + WMAX - 1 for pad <= 5
@@ -872,7 +875,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   floatx4v a0[12], a1[12];
   // fp32: a[u] = channels 16u + 4lq .. +3; X3: a[2s + h] = channels 32s + 8lq + 4h .. +3
   auto load = [&](int r, floatx4v (&a)[12]) {
-    const bool ok = r >= 0 && r < Hin && gx >= 0 && gx < Win;
+    const bool ok = !(TF2_ABL & 4) && r >= 0 && r < Hin && gx >= 0 && gx < Win;
     const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? gx : 0)) * Cin + (X3 ? 8 : 4) * lq;
 #pragma unroll
     for (int u = 0; u < 12; ++u) {
@@ -882,7 +885,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   };
   // the two rows completed by input row r (emitted from the block's run on)
   auto emit = [&](int r) {
-    if (r < r0) return;
+    if (r < r0 || (TF2_ABL & 2)) return;
     for (int h = 0; h < 2; ++h) {
       const int Y = 2 * r - pad + h;
       if (Y < 0 || Y >= Hout) continue;
@@ -909,7 +912,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
     floatx4v acc[5];
 #pragma unroll
     for (int ky = 0; ky < 5; ++ky) acc[ky] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    if (X3 && r >= 0 && r < Hin) {
+    if (X3 && !(TF2_ABL & 1) && r >= 0 && r < Hin) {
 #pragma unroll
       for (int sx = 0; sx < 6; ++sx) {
         if (sx < S) {
