@@ -247,22 +247,6 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 // into two patch buffers); one barrier per unit.  The output leaves in one burst per unit after
 // the MFMAs: streaming it out under them (one store per MFMA group, or two 4-wave blocks per CU
 // drifting apart, or waves 4-7 storing a phase late) measured slower (r03zf-r03zj).
-#ifndef EC3_STAMP
-#define EC3_STAMP 0  // diagnostic build: per-wave phase cycles of the last launch (tools/ec3_stamp.py)
-#endif
-#if EC3_STAMP
-__device__ unsigned long long ec3_stamps[256 * 8 * 8];
-#define EC3_T(k)                                                 \
-  do {                                                           \
-    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
-    ts_[k] += t1_ - t0_;                                         \
-    t0_ = t1_;                                                   \
-  } while (0)
-#else
-#define EC3_T(k) \
-  do {           \
-  } while (0)
-#endif
 constexpr int EC3_S = 3;
 constexpr int EC3_KP = 32 * EC3_S;       // k columns of the B planes (96)
 constexpr int EC3_PL = SEG * EC3_KP;     // bf16 per plane
@@ -347,9 +331,6 @@ __global__ void __launch_bounds__(512, 1)
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) ob[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-#if EC3_STAMP
-  unsigned long long ts_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0_ = __builtin_amdgcn_s_memtime();
-#endif
   int it = 0;
   for (long long u = u0; u < g.units; u += gs, ++it) {
 #pragma unroll
@@ -358,14 +339,10 @@ __global__ void __launch_bounds__(512, 1)
       for (int j = 0; j < NTW; ++j) asm volatile("" ::"v"(ob[t][j]));  // keeps `ob` apart from `acc`
     // planes(u) and patch(u + gs) are in LDS; every read of plane buffer (it + 1) & 1 and patch
     // buffer it & 1 (the previous iteration's) is done
-    EC3_T(0);
     __syncthreads();
-    EC3_T(1);
     const long long u2 = u + 2 * gs;
     edge_patch_load(g, pm, min(u2, ulast), pr);
-    EC3_T(2);
     build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);
-    EC3_T(3);
     const __bf16* planes = bpl + (it & 1) * 3 * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
@@ -394,9 +371,7 @@ __global__ void __launch_bounds__(512, 1)
     }
     // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration),
     // before this unit's global stores: waiting for its loads then never waits for them
-    EC3_T(4);
     edge_patch_store<512>(g, pr, lds + (it & 1) * bufsz, tid);
-    EC3_T(5);
     // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li).  The stored values
     // stay in registers of their own (`ob`, live across the unit loop): overwriting a store's data
     // registers waits for the store
@@ -411,7 +386,6 @@ __global__ void __launch_bounds__(512, 1)
           ob[t][j][r] = (relu && !(x > 0.f)) ? 0.f : x;  // branch-free ReLU
         }
     }
-    EC3_T(6);
     const int seg = (int)(u % g.units_per_row);
     const long long rr = u / g.units_per_row;
     float* yb = y + (rr / g.Ho) * ys_n + (rr % g.Ho) * ys_h + nbase + 4 * lq;
@@ -423,12 +397,7 @@ __global__ void __launch_bounds__(512, 1)
         for (int j = 0; j < NTW; ++j) *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = ob[t][j];
       }
     }
-    EC3_T(7);
   }
-#if EC3_STAMP
-  if (lane == 0 && blockIdx.x < 256)
-    for (int q = 0; q < 8; ++q) ec3_stamps[(blockIdx.x * 8 + w) * 8 + q] = ts_[q];
-#endif
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -786,9 +755,6 @@ __global__ void __launch_bounds__(64 * NWV, 2)
 #define TF2_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) on the input-row kernel
 #endif
 constexpr int TF2_RS = 8;  // ring slots: rows 2r - pad - 2 .. 2r - pad + k - 1 in flight
-#ifndef TF2_ABL
-#define TF2_ABL 0  // ablations (timing only): 1 no MFMAs, 2 no emission, 4 no input loads
-#endif
 constexpr int TF2_HALO = 2;  // input columns loaded left of a column segment (k <= 5, pad >= 0)
 // input columns a segment owns when the row is wider than the block (WMAX = 128): its output
 // columns need input columns up to (2 (sg + 1) wseg - 1 + pad) / 2 <= base + WMAX - 1 for pad <= 5
@@ -875,7 +841,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   floatx4v a0[12], a1[12];
   // fp32: a[u] = channels 16u + 4lq .. +3; X3: a[2s + h] = channels 32s + 8lq + 4h .. +3
   auto load = [&](int r, floatx4v (&a)[12]) {
-    const bool ok = !(TF2_ABL & 4) && r >= 0 && r < Hin && gx >= 0 && gx < Win;
+    const bool ok = r >= 0 && r < Hin && gx >= 0 && gx < Win;
     const float* xr = xn + ((size_t)(ok ? r : 0) * Win + (ok ? gx : 0)) * Cin + (X3 ? 8 : 4) * lq;
 #pragma unroll
     for (int u = 0; u < 12; ++u) {
@@ -885,7 +851,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
   };
   // the two rows completed by input row r (emitted from the block's run on)
   auto emit = [&](int r) {
-    if (r < r0 || (TF2_ABL & 2)) return;
+    if (r < r0) return;
     for (int h = 0; h < 2; ++h) {
       const int Y = 2 * r - pad + h;
       if (Y < 0 || Y >= Hout) continue;
@@ -912,7 +878,7 @@ __global__ void __launch_bounds__(64 * NWV, 1)
     floatx4v acc[5];
 #pragma unroll
     for (int ky = 0; ky < 5; ++ky) acc[ky] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    if (X3 && !(TF2_ABL & 1) && r >= 0 && r < Hin) {
+    if (X3 && r >= 0 && r < Hin) {
 #pragma unroll
       for (int sx = 0; sx < 6; ++sx) {
         if (sx < S) {
@@ -1152,8 +1118,3 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
   return IC_OK;
 }
 
-#if EC3_STAMP
-extern "C" int ic_edge_stamps(void* dst) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ec3_stamps), sizeof(ec3_stamps));
-}
-#endif

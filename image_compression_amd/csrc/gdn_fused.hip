@@ -477,19 +477,6 @@ __device__ __forceinline__ void bar_wait_lgkm() {
   __builtin_amdgcn_s_barrier();
 }
 
-#ifdef GDN_PROF  // per-phase timestamps (tools/gdn_prof.hip only)
-__device__ unsigned long long gdn_prof[256 * 8 * 16 * 6];
-#define GDN_MARK(it, ev)                                                                         \
-  do {                                                                                           \
-    if (blockIdx.x < 256 && (threadIdx.x & 63) == 0 && (it) < 16)                                \
-      gdn_prof[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 16 + (it)) * 6 + (ev)] =                 \
-          __builtin_amdgcn_s_memtime();                                                          \
-  } while (0)
-#else
-#define GDN_MARK(it, ev) \
-  do {                   \
-  } while (0)
-#endif
 
 // 8 waves, specialised (two per SIMD): waves 0-3 (group A) stage the tiles,
 // form dx by a GEMM with gamma held in VGPRs and copy it out; waves 4-7
@@ -578,15 +565,12 @@ __global__ void __launch_bounds__(512, 2)
       if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
       __builtin_amdgcn_s_barrier();  // B1
-      GDN_MARK(it, 0);
       first = false;
       const uint32_t nxt = tile + gridDim.x;
       float* xs = lds + buf * 3 * TILE;
       float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
       gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
-      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
-      GDN_MARK(it, 2);
       floatx4v acc[NTW];
 #pragma unroll
       for (int j = 0; j < NTW; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
@@ -620,7 +604,6 @@ __global__ void __launch_bounds__(512, 2)
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      GDN_MARK(it, 3);
       // dx = direct + 2 x dxg over the direct term (each element owned by one lane); m = 4lq + r
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
@@ -631,9 +614,7 @@ __global__ void __launch_bounds__(512, 2)
           gs[off] = gs[off] + 2.f * xs[off] * acc[j][r];
         }
       }
-      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
-      GDN_MARK(it, 5);
       store_tile<C, BM, NTA>(dx, tile * BM, P, gs, tid);
       buf ^= 1;
     }
@@ -668,16 +649,13 @@ __global__ void __launch_bounds__(512, 2)
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
-      GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
       if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
       gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
-      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
-      GDN_MARK(it, 2);
       if (t < C) {
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
@@ -706,10 +684,7 @@ __global__ void __launch_bounds__(512, 2)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0][j], acc[i][j], 0, 0, 0);
         }
       }
-      GDN_MARK(it, 3);
-      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
-      GDN_MARK(it, 5);
       if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
         const float* gsd = xs + 2 * TILE;
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
@@ -745,16 +720,13 @@ __global__ void __launch_bounds__(512, 2)
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
-      GDN_MARK(it, 0);
       const float* xs = lds + buf * 3 * TILE;
       const uint32_t m0 = tile * BM;
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
       if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
       gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
-      GDN_MARK(it, 1);
       bar_wait_lgkm();  // B2
-      GDN_MARK(it, 2);
       if (t < C) {
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) db += qs[swz<C>(m, t)];
@@ -794,10 +766,7 @@ __global__ void __launch_bounds__(512, 2)
         pin_acc<NTW * KT>(&dg[0][0]);
         __builtin_amdgcn_sched_barrier(0);
       }
-      GDN_MARK(it, 3);
-      GDN_MARK(it, 4);
       bar_wait_lgkm();  // B3
-      GDN_MARK(it, 5);
       if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
         const float* gsd = xs + 2 * TILE;
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;

@@ -57,28 +57,61 @@ def teardown():
         dist.destroy_process_group()
 
 
-def wrap(model, device, bucket_cap_mb=12.0):
+def _joined_allreduce_hook(streams, bucket):
+    """DDP comm hook: the bucket's all-reduce after every stream that produces gradients.
+
+    The reducer calls a hook when the last gradient of a bucket is accumulated, on that
+    gradient's stream; RCCL then orders the collective after that stream only.  With the
+    hyperprior on its side stream a bucket can mix gradients finished on both streams, so the
+    current stream first waits for the other one (an event at its tail: everything the
+    autograd engine has queued on it so far, which includes the bucket's own gradients).
+    Then the default hook: divide by the world size, all-reduce (SUM) the bucket in place."""
+    from torch.distributed.algorithms.ddp_comm_hooks.default_hooks import allreduce_hook
+    cur = torch.cuda.current_stream()
+    for s in streams:
+        if s != cur:
+            cur.wait_stream(s)
+    return allreduce_hook(None, bucket)
+
+
+def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
     """DDP over the model.  12 MB buckets ~ one bucket per transform
     (g_s 11.6 MB, h_s+EM 8.7 MB, h_a 8.7 MB, g_a 11.6 MB): the
     first all-reduce starts as soon as g_s's gradients are ready and overlaps
     the rest of the backward.  Gradients are views into the buckets (no copy).
 
-    The one place that decides the hyperprior side stream under data parallelism:
-    off.  DDP keeps the AccumulateGrad nodes it made at wrap time (on the current
-    stream) for the model's life, and its bucket all-reduce waits only for the
-    stream that readied the bucket; with the hyperprior's backward on a second
-    stream a bucket would mix gradients finished on two streams with no per-bucket
-    stream join.  The side stream is worth ~1 % of a C2 step at one rank
-    (14.39 -> 14.24-14.29 ms); under DDP every rank runs the
-    single-stream step, bitwise the same arithmetic."""
+    The hyperprior side stream stays on under DDP (concurrent=True, on GPUs), so every rank
+    runs the step bench.py measures at one rank.  Two things make that safe:
+    * the hyperprior parameters' AccumulateGrad nodes are made on the side stream before DDP
+      takes them (DDP keeps the nodes it finds at construction for the model's life; made on
+      the main stream, they would accumulate the side stream's gradients there, a cross-stream
+      use of the gradient's memory the caching allocator is not told about);
+    * a comm hook (_joined_allreduce_hook) joins both streams before each bucket's all-reduce.
+    concurrent=False runs the single-stream step (bitwise the same arithmetic)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return model
-    if hasattr(model, "concurrent_hyperprior"):
-        model.concurrent_hyperprior = False
     from torch.nn.parallel import DistributedDataParallel as DDP
+    conc = (concurrent and device.type == "cuda" and getattr(model, "concurrent_hyperprior", False)
+            and hasattr(model, "hyperprior_modules"))
+    if hasattr(model, "concurrent_hyperprior"):
+        model.concurrent_hyperprior = conc
+    keep = []
+    if conc:
+        from .modelling.meta_arch.bmshl2018 import side_stream
+        main = torch.cuda.current_stream(device)
+        side = side_stream(device)
+        with torch.cuda.stream(side):
+            for m in model.hyperprior_modules():
+                for p in m.parameters():
+                    if p.requires_grad:
+                        keep.append(p.view_as(p).grad_fn.next_functions[0][0])  # AccumulateGrad, side stream
     ids = [device.index] if device.type == "cuda" else None
-    return DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
-               broadcast_buffers=False)
+    ddp = DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+              broadcast_buffers=False)
+    if conc:
+        ddp.register_comm_hook([main, side], _joined_allreduce_hook)
+    del keep  # DDP holds the nodes now
+    return ddp
 
 
 def shard(t, rank, world):

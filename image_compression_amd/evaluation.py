@@ -161,18 +161,28 @@ class GraphForward:
 class Evaluator:
     """engine/evaluator.py:44-123 without the data loader / file outputs:
     run_eval(batches) over an iterable of [N,3,H,W] images in [0,1].  graph=True replays one
-    captured forward per input shape (GraphForward) instead of launching it eagerly."""
+    captured forward per input shape (GraphForward) instead of launching it eagerly;
+    weight_cache=False re-packs the weights on every eager forward (functional.weight_cache)."""
 
-    def __init__(self, model, device=None, graph=False):
+    def __init__(self, model, device=None, graph=False, weight_cache=True):
         self.model = model
         self.device = device
         self.monitor = Monitor(model.loss_names)
         self.graph = graph
+        self.weight_cache = weight_cache
         self._graphs = {}
+        self._graph_ptrs = None
 
     def _forward(self, imgs):
         if not (self.graph and imgs.is_cuda):
             return self.model(imgs)
+        # a captured graph holds raw device pointers to the parameters and buffers: if any of
+        # them was reallocated since capture (load_state_dict(assign=True), .to(...), a rebuilt
+        # module), replay would read freed memory, so the graphs are dropped and recaptured
+        ptrs = tuple(t.data_ptr() for t in list(self.model.parameters()) + list(self.model.buffers()))
+        if ptrs != self._graph_ptrs:
+            self._graphs.clear()
+            self._graph_ptrs = ptrs
         key = (tuple(imgs.shape), imgs.device)
         g = self._graphs.get(key)
         if g is None:
@@ -187,7 +197,7 @@ class Evaluator:
         self.monitor.reset()
         # eager forwards reuse the weight packs and GDN re-parameterisations across images (the
         # weights are constant here); captured graphs hold their launches already
-        scope = F.weight_cache() if not self.graph else contextlib.nullcontext()
+        scope = F.weight_cache() if (self.weight_cache and not self.graph) else contextlib.nullcontext()
         try:
             with scope:
                 for imgs in batches:

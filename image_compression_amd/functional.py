@@ -200,13 +200,17 @@ MATH = {"fp32": 0, "bf16": 1, "fp32_split": 2}
 
 
 # ---------------------------------------------------------- eval-mode weight caching
-# Inside `weight_cache()` (Evaluator.run_eval, GraphForward), forwards without autograd keep each
+# Inside `weight_cache()` (Evaluator.run_eval's eager path; GraphForward does not enter it: a
+# captured graph already holds its pack launches), forwards without autograd keep each
 # conv weight's MFMA pack in a workspace of its own and skip the pack launch while the weight is
 # unchanged (include/imgcomp.h IC_MATH_WPACKED), and NonNegativeParam keeps its re-parameterised
 # value: the eval forward then launches only the layer kernels.  An entry is valid for the same
 # tensor object (weakref) at the same version counter (every in-place update bumps it: torch ops,
 # load_state_dict's copy_, and solver.AdamW, which bumps it after its kernel) on the same stream
 # (the pack workspace also holds the split-K partials) and, for packs, the same operand geometry.
+# The stream is keyed by its raw handle: a stream destroyed inside one scope whose handle is reused
+# by a new stream would find the old entry, but the weakref and version checks still decide a hit,
+# and every entry is dropped when the outermost scope exits.
 IC_MATH_WPACKED = 4
 _WCACHE = {}
 _WCACHE_LOCK = threading.Lock()

@@ -2,8 +2,12 @@
 
 y = x / sqrt(beta + conv1x1(x^2, gamma))   (inverse: x * sqrt(...); relu: ReLU first)
 gamma, beta are re-parameterised by NonNegativeParam: max(p, bound)^2 - pedestal.
-The 1x1 "conv" is a CxC GEMM on fp32 MFMA with x^2 formed in the operand load
-and the divide fused in the epilogue (csrc/gdn.hip)."""
+The 1x1 "conv" is a CxC GEMM with x^2 formed in the operand load and the x * norm^-1/2
+epilogue fused (csrc/gdn_fused.hip): in the default fp32_split arithmetic the forward is
+gdn_fwd_x3s_kernel (Gamma x^2 on the bf16 MFMA through the exact three-term split) and the
+backward gdn_bwd_fused_kernel<C, true> (split dGamma GEMM, fp32-MFMA dx GEMM, dbeta and the
+producing conv's bias column sums in the same pass); COMPUTE_DTYPE "fp32" runs the fp32-MFMA
+forms, and shapes outside the fused kernels' layouts the generic csrc/gdn.hip kernels."""
 import torch
 import torch.nn as nn
 

@@ -36,7 +36,7 @@ class _StreamEdge(torch.autograd.Function):
         return g, None
 
 
-def _side_stream(device):
+def side_stream(device):
     """One high-priority side stream per device for the hyperprior branch."""
     k = device.index if device.index is not None else torch.cuda.current_device()
     if k not in _SIDE:
@@ -64,6 +64,12 @@ class Compressor2018(nn.Module):
         # stream, concurrent with the synthesis transform (see forward)
         self.concurrent_hyperprior = True
 
+    def hyperprior_modules(self):
+        """The modules whose forward, and so whose backward, run on the hyperprior side stream
+        when concurrent_hyperprior is on (h_a, the factorized model, h_s, the conditional
+        model): their parameters' gradients are produced on that stream (distributed.wrap)."""
+        return [self.prior_analysis, self.entropy_model, self.prior_synthesis, self.conditional_model]
+
     def forward(self, x):
         if self.training:
             _noise.begin_step(x.device)  # fresh Philox counters for this step
@@ -86,7 +92,7 @@ class Compressor2018(nn.Module):
             # backward on the same streams (the small hyperprior kernels hide under g_s's).
             # Same kernels, same draws in the same order (z, then y): bitwise the serial result.
             main = torch.cuda.current_stream(x.device)
-            side = _side_stream(x.device)
+            side = side_stream(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 y.record_stream(side)

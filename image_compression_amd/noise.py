@@ -45,6 +45,7 @@ def _st():
         _state.seed = None
         _state.dev = {}       # device -> int64[2] {seed, base} tensor
         _state.offset = {}    # device -> counters drawn so far this step
+        _state.rank = {}      # device -> the data-parallel rank its key was made for
         _state.queue = []
     return _state
 
@@ -84,14 +85,22 @@ def process_key(seed):
 
 def device_state(device):
     """The {seed, base} tensor of `device` (created on first use; the key folds in this
-    process's data-parallel rank, see rank_key)."""
+    process's data-parallel rank, see rank_key).  A state created before the process group
+    was initialised carries rank 0's key; if the rank has changed since, the key word is
+    rewritten in place (the base, i.e. the counters already drawn, is kept), so no two ranks
+    ever share a stream because of when the first draw happened."""
     s = _st()
     k = _key(device)
+    rank = _dist_rank()
     if k not in s.dev:
         if s.seed is None:
             s.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        s.dev[k] = torch.tensor([process_key(s.seed), 0], dtype=torch.int64, device=torch.device(*k))
+        s.dev[k] = torch.tensor([rank_key(s.seed, rank), 0], dtype=torch.int64, device=torch.device(*k))
         s.offset[k] = 0
+        s.rank[k] = rank
+    elif s.rank.get(k) != rank:
+        s.dev[k][0].fill_(rank_key(s.seed, rank))
+        s.rank[k] = rank
     return s.dev[k]
 
 
@@ -122,6 +131,7 @@ def reseed(seed=None):
     s.seed = None if seed is None else int(seed)
     s.dev = {}
     s.offset = {}
+    s.rank = {}
 
 
 def pop_injected():

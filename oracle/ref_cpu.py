@@ -287,12 +287,17 @@ def cdf_logits(P, x, n_layers=None, prefix="entropy_model._cdf_estimator.layers.
     return h.view(N, *sp, C).permute(*order)
 
 
-def factorized(P, z, u=None, train=True, bin_=1.0):
+def factorized(P, z, u=None, train=True, bin_=1.0, sym=None):
     """entropy_model.py:204-269 EntropyModel.forward: noise (u - bin/2, :230) or
-    round (:234); likelihood via the detached sign trick (:259-269)."""
+    round (:234); likelihood via the detached sign trick (:259-269).  `sym` (eval only, test
+    infrastructure): the symbols to use in place of round(z) — another implementation's
+    rounding, so that a symbol sitting within float error of a .5 boundary (a tie, checked by
+    the caller) does not decide the comparison of everything downstream."""
     half = bin_ / 2
     if train:
         q = z + (u - half).detach()
+    elif sym is not None:
+        q = z * 0 + torch.as_tensor(sym).to(z.dtype)  # zero gradient, like torch.round
     else:
         q = torch.round(z)
     lower = cdf_logits(P, q - half)
@@ -312,12 +317,14 @@ def normal_cdf(v):
     return 0.5 * (1 + torch.erf(v * 1.0 / math.sqrt(2)))
 
 
-def conditional(y, scale, u=None, train=True, kind="laplace", mean=0, bin_=1.0):
+def conditional(y, scale, u=None, train=True, kind="laplace", mean=0, bin_=1.0, sym=None):
     """entropy_model.py:280-352: noise/round then
-    p = F((half - |y~ - mean|)/scale) - F((-half - |y~ - mean|)/scale)."""
+    p = F((half - |y~ - mean|)/scale) - F((-half - |y~ - mean|)/scale).  `sym`: as factorized."""
     half = bin_ / 2
     if train:
         q = y + (u - half).detach()
+    elif sym is not None:
+        q = y * 0 + torch.as_tensor(sym).to(y.dtype)
     else:
         q = torch.round(y)
     a = torch.abs(q - mean)
@@ -448,17 +455,18 @@ def ms_ssim_metric_db(a, b, max_val=255.0, size=11, sigma=1.5, k1=0.01, k2=0.03,
 def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             loss_names=("MSE",), lam=256.0, ssim_log=True,
             strides=(2, 2, 2, 2), hp_strides=(1, 2, 2), hp_kernels=(3, 5, 5), relu_ctl=None, bin_=1.0,
-            bf16=None):
+            bf16=None, sym_z=None, sym_y=None):
     """modelling/meta_arch/bmshl2018.py:68-98 Compressor2018.forward.
     Returns dict of intermediates and the loss dict.  bf16: per-layer bf16 operand
-    emulation of the main transforms' GEMMs (_conv; None = exact)."""
+    emulation of the main transforms' GEMMs (_conv; None = exact).  sym_z / sym_y (eval):
+    symbols fed in place of round(z) / round(y) (see factorized)."""
     N, C, H, W = x.shape
     num_pixels = N * H * W
     y = analysis(P, x, strides, bf16=bf16)
     z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl)
-    z_tilde, p_z, ce_z = factorized(P, z, u_z, train, bin_)
+    z_tilde, p_z, ce_z = factorized(P, z, u_z, train, bin_, sym=sym_z)
     sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl)
-    y_tilde, p_y = conditional(y, sigma, u_y, train, cond, bin_=bin_)
+    y_tilde, p_y = conditional(y, sigma, u_y, train, cond, bin_=bin_, sym=sym_y)
     ce_y = ce_loss(p_y)
     x_raw = synthesis(P, y_tilde, strides, bf16=bf16)
     x_tilde = lower_bound(upper_bound(x_raw, 1.0), 0.0)

@@ -69,6 +69,27 @@ def assert_close(a, b, rtol=1e-4, name=""):
             f"at {np.unravel_index(i, a.shape)} a={a.flat[i]:.6g} b={b.flat[i]:.6g} atol={atol:.3e}")
 
 
+def check_round_ties(sym, pre, tau=1e-4, name=""):
+    """Eval-mode rounding (entropy_model.py:234,337: torch.round, half to even): every symbol
+    of `sym` (the HIP path's) must equal round(`pre`) (the reference's / oracle's pre-round
+    value), except where `pre` sits on a tie: within tau * max|pre| of a .5 boundary, where two
+    correct fp32 evaluations may round either way; there the two symbols must be
+    the two neighbours of the boundary.  Returns the number of such flips."""
+    sym = np.asarray(sym, dtype=np.float64)
+    pre = np.asarray(pre, dtype=np.float64)
+    assert sym.shape == pre.shape, (name, sym.shape, pre.shape)
+    assert np.array_equal(sym, np.round(sym)), f"{name}: symbols are not integers"
+    diff = sym != np.round(pre)
+    if diff.any():
+        lim = tau * max(float(np.abs(pre).max()), 1e-30)
+        d = np.abs(np.abs(pre - np.floor(pre)) - 0.5)[diff]
+        assert float(d.max()) <= lim, (f"{name}: {int(diff.sum())} symbol(s) differ, one {float(d.max()):.3e} "
+                                       f"from a .5 boundary > {lim:.3e}")
+        assert np.all(np.abs(sym[diff] - np.round(pre[diff])) == 1), name
+        assert np.all(np.abs(sym[diff] - pre[diff]) <= 0.5 + lim), name
+    return int(diff.sum())
+
+
 class HipReluMasks:
     """Records, in call order, the gradient masks (input > 0) of the HIP model's
     hyperprior ReLUs (the only ReLUs of Compressor2018), for the oracle's

@@ -1,9 +1,10 @@
 """The data-parallel path with the HIP kernels: two ranks (gloo over GPU
 tensors, sharing the box's one GPU — the RCCL path needs one GPU per rank),
 each on half the batch, average to the single-process gradient of the whole
-batch (injected noise, fixed weights) -- under DistributedDataParallel (the
-single-stream step D.wrap selects) and through TrainStep's flat gradient
-buffer and one all-reduce (with the hyperprior side stream).  The ranks'
+batch (injected noise, fixed weights) -- under DistributedDataParallel with the
+hyperprior side stream (D.wrap's comm hook joins both streams before each bucket's
+all-reduce; bitwise equal to the single-stream DDP step) and through TrainStep's flat
+gradient buffer and one all-reduce.  The ranks'
 training-noise keys differ (noise.rank_key).  Unmeasured on RCCL hardware:
 the box has one GPU."""
 import os
@@ -36,22 +37,28 @@ def _inputs():
 def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), IMGCOMP_DIST_BACKEND="gloo")
+    import warnings
+    # as tests/conftest.py: a gradient accumulated on another stream than its producer's is an error
+    warnings.filterwarnings("error", message="(?s).*AccumulateGrad node's stream does not match")
     from image_compression_amd import distributed as D
     from image_compression_amd import injected_noise, modelling
     from image_compression_amd import noise
     from image_compression_amd.step import TrainStep
     _, _, dev = D.setup()
-    torch.manual_seed(0)
-    model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev, bucket_cap_mb=4.0)
-    assert model.module.concurrent_hyperprior is False     # D.wrap decides the side stream under DDP
     x, uz, uy = (D.shard(t, rank, world).to(dev) for t in _inputs())
-    for _ in range(2):       # DDP raises on the 2nd iteration if a parameter went unused
-        model.zero_grad(set_to_none=True)
-        with injected_noise([uz, uy]):
-            _, losses = model(x)
-        losses["total_loss"].backward()
-    torch.cuda.synchronize()
-    ddp_grads = {n: p.grad.detach().cpu() for n, p in model.module.named_parameters()}
+    ddp_grads = {}
+    for conc in (True, False):
+        torch.manual_seed(0)
+        model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev, bucket_cap_mb=4.0, concurrent=conc)
+        assert model.module.concurrent_hyperprior is conc     # the side stream stays on under DDP
+        for _ in range(3):       # DDP raises on the 2nd iteration if a parameter went unused; buckets rebuilt
+            model.zero_grad(set_to_none=True)
+            with injected_noise([uz, uy]):
+                _, losses = model(x)
+            losses["total_loss"].backward()
+        torch.cuda.synchronize()
+        ddp_grads[conc] = {n: p.grad.detach().cpu() for n, p in model.module.named_parameters()}
+        del model, losses
     # the hipGraph-capable step without DDP: gradients as views of one flat buffer, one
     # all-reduce after the backward, hyperprior side stream on
     torch.manual_seed(0)
@@ -68,8 +75,8 @@ def _worker(rank, world, port, outdir):
     keys = [torch.zeros_like(key) for _ in range(world)]
     torch.distributed.all_gather(keys, key)
     if rank == 0:
-        torch.save({"ddp": ddp_grads, "flat": flat_grads, "keys": [int(k) for k in keys],
-                    "seed": noise._st().seed}, os.path.join(outdir, "g.pt"))
+        torch.save({"ddp": ddp_grads[True], "ddp_serial": ddp_grads[False], "flat": flat_grads,
+                    "keys": [int(k) for k in keys], "seed": noise._st().seed}, os.path.join(outdir, "g.pt"))
     D.teardown()
 
 
@@ -89,6 +96,9 @@ def test_ddp_two_ranks_match_full_batch(tmp_path):
     with injected_noise([uz, uy]):
         _, losses = model(x)
     losses["total_loss"].backward()
+    # the concurrent-hyperprior DDP step (the measured step) is bitwise the single-stream one
+    for n in res["ddp"]:
+        assert torch.equal(res["ddp"][n], res["ddp_serial"][n]), n
     for kind in ("ddp", "flat"):
         g = res[kind]
         worst = max((rel_err(g[n], p.grad.cpu()), n) for n, p in model.named_parameters())

@@ -124,7 +124,17 @@ def _key_worker(rank, world, port, outdir):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from image_compression_amd import distributed as D
     from image_compression_amd import noise
+    # a device state made before the process group exists carries rank 0's key ...
+    noise.reseed(99)
+    dev = torch.device("cpu", 0)
+    early = int(noise.device_state(dev)[0])
+    assert early == noise.rank_key(99, 0)
     D.setup("gloo", device_type="cpu")
+    # ... and is re-keyed for this rank at its next use (counters kept)
+    noise.device_state(dev)[1] += 12
+    st, off = noise.philox_stream(8, dev)
+    assert int(st[0]) == noise.rank_key(99, rank) and int(st[1]) == 12 and off == 0
+    noise.reseed()
     torch.manual_seed(0)                       # every rank seeds alike, as bench.py does
     seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     keys = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
