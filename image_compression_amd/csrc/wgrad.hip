@@ -12,6 +12,7 @@
 // they sit in NHWC memory); a half-wave reads 32 consecutive floats of one row
 // per operand fragment (ds_read_b32, conflict-free).
 #include "gemm.h"
+#include <algorithm>
 
 #ifndef WG_X3_TWO
 #define WG_X3_TWO 0  // split wgrad: 1 = two blocks per CU (swizzled unpadded rows), 0 = one (padded rows)
@@ -1004,6 +1005,54 @@ __global__ void wg_reduce2_kernel(const float* p2, int G, long long total, int C
   }
 }
 
+// The final level of the reduction through LDS: out[g][c][kk] is the weight's PyTorch layout (taps
+// fastest), while the partials run channels fastest, so a thread per (g, t, c) writes 4 B every kk
+// floats -- each wave's stores then touch 64 different lines (15.7x the compulsory write bytes,
+// r04b).  Here block (g, cb) sums the partials of channels [cb CB, cb CB + CB) of row g over every
+// tap in the same fixed order (reads coalesced along c), transposes them in LDS to [c][kk] and
+// writes out[g][cb CB .. + CB][0 .. kk) as one contiguous run.  Bitwise the result of
+// wg_reduce_kernel / wg_reduce2_kernel.
+__global__ void __launch_bounds__(256) wg_reduce_t_kernel(const WgRed r, int CB) {
+  extern __shared__ float row[];  // [CB][kk]
+  const int g = blockIdx.x, c0 = blockIdx.y * CB, cn = min(CB, r.Cx - c0);
+  const long long sstride = (long long)r.Tp * r.Cg * r.ncols;
+  for (int idx = threadIdx.x; idx < r.T * cn; idx += blockDim.x) {
+    const int t = idx / cn, cl = idx - t * cn, c = c0 + cl;
+    const int tp = r.generic ? 0 : t;
+    const int col = r.generic ? t * r.Cx + c : c;
+    const float* src = r.partial + ((long long)tp * r.Cg + g) * r.ncols + col;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int sp = 0;
+    for (; sp + 3 < r.nsplit; sp += 4) {
+      a0 += src[(long long)sp * sstride];
+      a1 += src[(long long)(sp + 1) * sstride];
+      a2 += src[(long long)(sp + 2) * sstride];
+      a3 += src[(long long)(sp + 3) * sstride];
+    }
+    for (; sp < r.nsplit; ++sp) a0 += src[(long long)sp * sstride];
+    row[cl * r.kk + r.kk_of_t[t]] = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
+  float* o = r.out + ((long long)g * r.Cx + c0) * r.kk;
+  for (int j = threadIdx.x; j < cn * r.kk; j += blockDim.x) o[j] = row[j];
+}
+
+__global__ void __launch_bounds__(256) wg_reduce2_t_kernel(const float* p2, int G, long long total, const WgRed r,
+                                                           float* out, int CB) {
+  extern __shared__ float row[];  // [CB][kk]
+  const int g = blockIdx.x, c0 = blockIdx.y * CB, cn = min(CB, r.Cx - c0);
+  for (int idx = threadIdx.x; idx < r.T * cn; idx += blockDim.x) {
+    const int t = idx / cn, cl = idx - t * cn;
+    const long long i = ((long long)g * r.T + t) * r.Cx + c0 + cl;
+    float v = 0.f;
+    for (int q = 0; q < G; ++q) v += p2[(long long)q * total + i];
+    row[cl * r.kk + r.kk_of_t[t]] = v;
+  }
+  __syncthreads();
+  float* o = out + ((long long)g * r.Cx + c0) * r.kk;
+  for (int j = threadIdx.x; j < cn * r.kk; j += blockDim.x) o[j] = row[j];
+}
+
 template <int BM, int BN, int WM, int WN, bool GEN>
 int wg_launch_t(const WgDesc& d, hipStream_t s) {
   const int Tp = GEN ? 1 : d.T;
@@ -1157,6 +1206,9 @@ int colsum_blocks(long long rows) {
 }  // namespace
 
 constexpr int WG_SPG = 32;  // splits summed per thread in the first reduce level
+#ifndef WG_REDUCE_T
+#define WG_REDUCE_T 1  // last reduce level through an LDS transpose (coalesced [g][c][kk] rows)
+#endif
 
 size_t wg_plan(WgDesc& d) {
   // split kernel: NHWC, 4-aligned channel rows, 192-wide tiles (wg_x3_kernel)
@@ -1257,11 +1309,25 @@ int wg_reduce(const WgDesc& d, float* out, const int* kk_of_t, int kk, hipStream
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) return IC_OK;
+  // the last level transposes [CB channels][kk] slices of each g row through LDS (wg_reduce_t_kernel):
+  // CB sized for about two (t, c) elements per thread
+  const int CB = std::max(1, std::min(d.Cx, 512 / std::max(1, d.T)));
+  const size_t rowb = (size_t)CB * kk * sizeof(float);
+  const bool tr = WG_REDUCE_T && rowb <= 64 * 1024 && kk >= d.T;
+  const dim3 tgrid((unsigned)d.Cg, (unsigned)((d.Cx + CB - 1) / CB));
+  if (r.G == 1 && tr) {
+    hipLaunchKernelGGL(wg_reduce_t_kernel, tgrid, dim3(256), rowb, s, r, CB);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   hipLaunchKernelGGL(wg_reduce_kernel, dim3((unsigned)blocks, r.G), dim3(256), 0, s, r);
   IC_CHECK_LAUNCH();
   if (r.G > 1) {
-    hipLaunchKernelGGL(wg_reduce2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p2, r.G, total, d.Cx, d.T, kk,
-                       r, out);
+    if (tr)
+      hipLaunchKernelGGL(wg_reduce2_t_kernel, tgrid, dim3(256), rowb, s, p2, r.G, total, r, out, CB);
+    else
+      hipLaunchKernelGGL(wg_reduce2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p2, r.G, total, d.Cx, d.T, kk,
+                         r, out);
     IC_CHECK_LAUNCH();
   }
   return IC_OK;

@@ -82,11 +82,13 @@ def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
 
     The hyperprior side stream stays on under DDP (concurrent=True, on GPUs), so every rank
     runs the step bench.py measures at one rank.  Two things make that safe:
-    * the hyperprior parameters' AccumulateGrad nodes are made on the side stream before DDP
-      takes them (DDP keeps the nodes it finds at construction for the model's life; made on
-      the main stream, they would accumulate the side stream's gradients there, a cross-stream
-      use of the gradient's memory the caching allocator is not told about);
-    * a comm hook (_joined_allreduce_hook) joins both streams before each bucket's all-reduce.
+    * the hyperprior parameters' AccumulateGrad nodes are made on the streams their gradients
+      are produced on (model.gradient_streams: the side stream, and the hyperprior convs'
+      weight-gradient stream) before DDP takes them (DDP keeps the nodes it finds at
+      construction for the model's life; made on the main stream, they would accumulate the
+      other streams' gradients there, a cross-stream use of the gradient's memory the caching
+      allocator is not told about);
+    * a comm hook (_joined_allreduce_hook) joins every such stream before each bucket's all-reduce.
     concurrent=False runs the single-stream step (bitwise the same arithmetic)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return model
@@ -95,21 +97,19 @@ def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
             and hasattr(model, "hyperprior_modules"))
     if hasattr(model, "concurrent_hyperprior"):
         model.concurrent_hyperprior = conc
-    keep = []
+    keep, streams = [], [torch.cuda.current_stream(device)] if conc else []
     if conc:
-        from .modelling.meta_arch.bmshl2018 import side_stream
-        main = torch.cuda.current_stream(device)
-        side = side_stream(device)
-        with torch.cuda.stream(side):
-            for m in model.hyperprior_modules():
-                for p in m.parameters():
+        for stream, params in model.gradient_streams(device):
+            streams.append(stream)
+            with torch.cuda.stream(stream):
+                for p in params:
                     if p.requires_grad:
-                        keep.append(p.view_as(p).grad_fn.next_functions[0][0])  # AccumulateGrad, side stream
+                        keep.append(p.view_as(p).grad_fn.next_functions[0][0])  # AccumulateGrad on `stream`
     ids = [device.index] if device.type == "cuda" else None
     ddp = DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
               broadcast_buffers=False)
     if conc:
-        ddp.register_comm_hook([main, side], _joined_allreduce_hook)
+        ddp.register_comm_hook(streams, _joined_allreduce_hook)
     del keep  # DDP holds the nodes now
     return ddp
 

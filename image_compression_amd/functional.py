@@ -282,11 +282,102 @@ def nonneg_cached(p, bound, pedestal):
     return e["val"]
 
 
+# ---------------------------------------------------------- weight gradients on a stream of their own
+# A conv whose forward runs on a stream registered here (the hyperprior side stream, see
+# Compressor2018) gets its weight / bias gradient as a separate autograd node whose forward, and so
+# whose backward, runs on the registered weight-gradient stream:
+#     y = Join(ConvData(x, w.detach(), b.detach()), WGrad(x, w, b))
+# WGrad is created first, so its sequence number is lower than ConvData's: when Join's gradient
+# arrives, the engine runs ConvData's backward (the input gradient, on the side stream) before
+# WGrad's (the weight gradient, on its own stream).  The hyperprior's backward chain -- the input
+# gradients that g_a's backward waits for -- then no longer queues behind its weight gradients,
+# which run beside the rest of the step.  The parameters' AccumulateGrad nodes are made on the
+# weight-gradient stream (the parameters enter the graph through WGrad), the end of backward joins
+# every leaf stream, and the arithmetic is the unsplit conv's (the same kernels on the same operands).
+_WG_STREAMS = {}   # producing stream handle -> the stream its convs' weight gradients run on
+_ZERO = {}         # device index -> a zero scalar (WGrad's output is an expanded view of it)
+
+
+def route_weight_gradients(stream, wstream):
+    """Convs run on `stream` compute their weight gradients on `wstream` (see above)."""
+    _WG_STREAMS[stream.cuda_stream] = wstream
+
+
+def _wgrad_stream(x, weight):
+    if not _WG_STREAMS or not x.is_cuda or not torch.is_grad_enabled() or not weight.requires_grad:
+        return None
+    return _WG_STREAMS.get(torch.cuda.current_stream(x.device).cuda_stream)
+
+
+class _ConvWGradFn(Function):
+    """The weight and bias gradient of a conv (WGrad above).  Forward: nothing (an expanded zero of
+    the conv output's shape); backward, on the stream the forward ran on: the wgrad kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, holder, conf, shape):
+        dev = x.device.index
+        if dev not in _ZERO:
+            _ZERO[dev] = torch.zeros((), device=x.device, dtype=torch.float32)
+        ctx.holder = holder
+        ctx.conf = conf
+        ctx.has_b = bias is not None
+        ctx.save_for_backward(x, weight)
+        return _ZERO[dev].expand(shape)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, w = ctx.saved_tensors
+        transposed, stride, padding, act, math = ctx.conf
+        cur = torch.cuda.current_stream(x.device)
+        x.record_stream(cur)   # x and the incoming gradient were allocated on the producing stream
+        gz.record_stream(cur)
+        gy = relu_bwd(ctx.holder["y"], gz) if act else gz
+        gy = _cl(gy)
+        ops, k = _lib.ops(), w.shape[2]
+        if transposed:
+            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, ctx.has_b, math)
+            _log_plan("conv_transpose2d_wgrad", x, gy, k, stride, padding, math)
+        else:
+            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, ctx.has_b, math)
+            _log_plan("conv2d_wgrad", x, gy, k, stride, padding, math)
+        return None, dw, (db if ctx.has_b else None), None, None, None
+
+
+class _JoinFn(Function):
+    """y, passing its gradient to both the input-gradient and the weight-gradient node."""
+
+    @staticmethod
+    def forward(ctx, y, z):
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def _deferred_wgrad(ws, data_fn, x, weight, bias, args, conf, shape):
+    ws.wait_stream(torch.cuda.current_stream(x.device))
+    holder = {}
+    with torch.cuda.stream(ws):
+        z = _ConvWGradFn.apply(x, weight, bias, holder, conf, shape)
+    y = data_fn.apply(x, weight.detach(), None if bias is None else bias.detach(), *args)
+    if conf[3]:
+        holder["y"] = y
+    return _JoinFn.apply(y, z)
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, act=0, math=0):
     """`math` (forward and input gradient): 0 fp32 (default), 1 bf16 operands with fp32
     accumulation, 2 fp32 by exact bf16 split (see MATH)."""
     if _wcache_on(x):
         return _cached_conv("conv2d_fwd_ws", x, weight, bias, (int(stride), int(padding), int(act)), math)
+    ws = _wgrad_stream(x, weight)
+    if ws is not None:
+        k = weight.shape[2]
+        N, _, H, W = x.shape
+        shape = (N, weight.shape[0], (H + 2 * padding - k) // stride + 1, (W + 2 * padding - k) // stride + 1)
+        return _deferred_wgrad(ws, Conv2dFn, x, weight, bias, (int(stride), int(padding), int(act), int(math)),
+                               (False, int(stride), int(padding), int(act), int(math)), shape)
     return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), int(act), int(math))
 
 
@@ -294,6 +385,15 @@ def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0
     if _wcache_on(x):
         return _cached_conv("conv_transpose2d_fwd_ws", x, weight, bias,
                             (int(stride), int(padding), int(output_padding), int(act)), math)
+    ws = _wgrad_stream(x, weight)
+    if ws is not None:
+        k = weight.shape[2]
+        N, _, H, W = x.shape
+        shape = (N, weight.shape[1], (H - 1) * stride - 2 * padding + k + output_padding,
+                 (W - 1) * stride - 2 * padding + k + output_padding)
+        return _deferred_wgrad(ws, ConvTranspose2dFn, x, weight, bias,
+                               (int(stride), int(padding), int(output_padding), int(act), int(math)),
+                               (True, int(stride), int(padding), int(act), int(math)), shape)
     return ConvTranspose2dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), int(act),
                                    int(math))
 

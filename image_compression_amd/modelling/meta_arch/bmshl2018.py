@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from ... import noise as _noise
-from ...functional import AbsFn
+from ...functional import AbsFn, route_weight_gradients
 from ..blocks import (ENTROPY_MODEL_REGISTRY, AnalysisTransform, HyperpriorAnalysisTransform,
                       HyperpriorSynthesisTransform, SynthesisTransform)
 from ..layers import LowerBound, UpperBound
@@ -17,6 +17,7 @@ from .build import META_ARCH_REGISTRY
 
 
 _SIDE = {}
+_WGRAD = {}
 
 
 class _StreamEdge(torch.autograd.Function):
@@ -37,11 +38,21 @@ class _StreamEdge(torch.autograd.Function):
 
 
 def side_stream(device):
-    """One high-priority side stream per device for the hyperprior branch."""
+    """One high-priority side stream per device for the hyperprior branch, and beside it a
+    normal-priority stream for the hyperprior convs' weight gradients (functional: convs run on the
+    side stream compute them there, off the chain of input gradients g_a's backward waits for)."""
     k = device.index if device.index is not None else torch.cuda.current_device()
     if k not in _SIDE:
         _SIDE[k] = torch.cuda.Stream(device=device, priority=-1)
+        _WGRAD[k] = torch.cuda.Stream(device=device, priority=0)
+        route_weight_gradients(_SIDE[k], _WGRAD[k])
     return _SIDE[k]
+
+
+def wgrad_stream(device):
+    """The stream the hyperprior convs' weight gradients run on (see side_stream)."""
+    side_stream(device)
+    return _WGRAD[device.index if device.index is not None else torch.cuda.current_device()]
 
 
 @META_ARCH_REGISTRY.register()
@@ -69,6 +80,17 @@ class Compressor2018(nn.Module):
         when concurrent_hyperprior is on (h_a, the factorized model, h_s, the conditional
         model): their parameters' gradients are produced on that stream (distributed.wrap)."""
         return [self.prior_analysis, self.entropy_model, self.prior_synthesis, self.conditional_model]
+
+    def gradient_streams(self, device):
+        """[(stream, parameters)]: the stream each hyperprior parameter's gradient is produced and
+        accumulated on when concurrent_hyperprior is on -- the convs' weights and biases on the
+        weight-gradient stream, the entropy models' parameters on the side stream (main-stream
+        parameters are not listed).  distributed.wrap makes their AccumulateGrad nodes there."""
+        convs = [p for blk in (self.prior_analysis, self.prior_synthesis) for m in blk.modules()
+                 if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)) for p in m.parameters(recurse=False)]
+        ids = {id(p) for p in convs}
+        rest = [p for m in self.hyperprior_modules() for p in m.parameters() if id(p) not in ids]
+        return [(wgrad_stream(device), convs), (side_stream(device), rest)]
 
     def forward(self, x):
         if self.training:

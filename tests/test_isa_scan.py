@@ -1,0 +1,35 @@
+"""The built library's gfx950 code objects carry no packed-fp32 VALU instruction
+(v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32), whose result a following instruction read stale
+when MFMA kernels shared the SIMD (the round-3 fact_bwd_k fault; tools/pk_hazard_probe.hip
+reproduces it in isolation).  Every source is built with -packed-fp32-ops disabled (csrc/Makefile);
+this scan catches a source, flag or inline asm that reintroduces one.  CPU only: it disassembles
+the in-tree libimgcomp.so (tools/isa_scan.py)."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "image_compression_amd", "lib", "libimgcomp.so")
+
+
+def _scanner():
+    spec = importlib.util.spec_from_file_location("isa_scan", os.path.join(ROOT, "tools", "isa_scan.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libimgcomp.so not built")
+def test_no_packed_fp32_valu_in_any_kernel():
+    scan = _scanner()
+    kernels = scan.disassemble(LIB)
+    # every kernel family of the hot path is in the library (the scan saw real code)
+    names = " ".join(kernels)
+    for fam in ("ig_kernel_x3d", "wg_x3d_kernel", "gdn_bwd_fused_kernel", "gdn_fwd_x3s_kernel", "fact_bwd_k",
+                "edge_conv_x3_kernel", "tconv_few2_kernel", "colsum_rows_kernel", "adamw_kernel"):
+        assert fam in names, fam
+    assert sum(len(v) for v in kernels.values()) > 100000
+    hits = {k: n for k, n in scan.count(kernels, r"v_pk_(add|mul|fma)_f32").items() if n}
+    assert not hits, f"packed-fp32 VALU in {len(hits)} kernels: " + ", ".join(
+        f"{k[:60]} ({n})" for k, n in sorted(hits.items(), key=lambda t: -t[1])[:8])

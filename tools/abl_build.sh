@@ -6,11 +6,12 @@
 set -e
 TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
-C=$R/image_compression_amd/csrc
+# SRC_ROOT: a patched copy of the tree's include/ and image_compression_amd/csrc/ (diagnostic variants)
+C=${SRC_ROOT:-$R}/image_compression_amd/csrc
 B=$R/tools/_abl/build_$TAG
 O=$R/tools/_abl/$TAG
 mkdir -p $B $O
-NOPK_SRCS=${NOPK_SRCS-"entropy elementwise msssim metrics optim igemm"}   # as the Makefile (override: NOPK_SRCS=...)
+NOPK_SRCS=${NOPK_SRCS-"igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics"}  # as the Makefile: all (override: NOPK_SRCS=...)
 for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics; do
   extra=""
   case " $NOPK_SRCS " in *" $f "*) extra="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
@@ -21,7 +22,7 @@ wait
 ls $B/*.o | wc -l | grep -qx 13 || { echo "abl_build: an object failed to build"; exit 1; }
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libimgcomp.so $B/*.o
 TORCH_DIR=$(python3 -c 'import os, torch; print(os.path.dirname(torch.__file__))')
-g++ -shared -o $O/libimgcomp_torch.so $C/build/torch_ops.o -L$O -limgcomp -L$TORCH_DIR/lib -ltorch -ltorch_cpu -lc10 \
+g++ -shared -o $O/libimgcomp_torch.so $R/image_compression_amd/csrc/build/torch_ops.o -L$O -limgcomp -L$TORCH_DIR/lib -ltorch -ltorch_cpu -lc10 \
   -lc10_hip -ltorch_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$TORCH_DIR/lib
 rm -rf $B
 echo built tools/_abl/$TAG/
