@@ -51,6 +51,11 @@ class ICAdamWTensor(ctypes.Structure):
                 ("n", c_ll), ("lr", c_float), ("weight_decay", c_float)]
 
 
+class ICNonNegTensor(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("out", ctypes.c_void_p), ("gout", ctypes.c_void_p), ("gin", ctypes.c_void_p),
+                ("n", ctypes.c_longlong), ("bound", ctypes.c_float), ("pedestal", ctypes.c_float)]
+
+
 class ICPlan(ctypes.Structure):
     _fields_ = [("kernel", c_int), ("bm", c_int), ("bn", c_int), ("ksplit", c_int), ("nsplit", c_int),
                 ("im2col", c_int), ("variant", c_int), ("blocks", c_ll)]
@@ -125,6 +130,7 @@ SIGNATURES = {
     "ic_psnr_ex": (c_int, [c_void, c_void, c_int, c_ll, c_float, c_void, c_void, c_size, c_void]),
     "ic_images_u8_to_input": (c_int, [c_void, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void, c_void, c_void,
                                       c_void]),
+    "ic_nonneg_multi": (c_int, [P(ICNonNegTensor), c_int, c_int, c_void]),
     "ic_adamw_step": (c_int, [P(ICAdamWTensor), c_int, ctypes.c_double, ctypes.c_double, c_float, c_float, c_ll,
                               c_void]),
     "ic_factorized_fwd": (c_int, [c_void, c_ll, c_int, P(ICFactParams), c_int, c_void, c_ull, c_ull, c_void, c_void, c_void]),

@@ -10,6 +10,10 @@
 #include "../../include/imgcomp.h"
 #include "gemm.h"
 
+#ifndef TAP_PARITY_ORDER
+#define TAP_PARITY_ORDER 0  // 1: stride-2 direct convs walk even kernel rows first, then odd (conv_impl)
+#endif
+
 thread_local ic_plan* g_plan_sink = nullptr;
 
 namespace {
@@ -174,7 +178,13 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   P.T = k * k;
   int ky[IC_MAXT], kx[IC_MAXT];
   for (int t = 0; t < P.T; ++t) {
-    ky[t] = t / k; kx[t] = t % k;
+    // TAP_PARITY_ORDER: kernel rows 0, 2, 4, 1, 3 (k = 5).  Tap row ky reads input rows 2y + ky - pad,
+    // so even and odd kernel rows read disjoint rows: taken parity by parity, the input rows a
+    // channel chunk's taps read stay in the XCD's L2 across those taps (r05a: no gain on the
+    // split kernels, which are not bound by those bytes)
+    const int r = t / k, ne = (k + 1) / 2;
+    ky[t] = (stride == 2 && TAP_PARITY_ORDER) ? (r < ne ? 2 * r : 2 * (r - ne) + 1) : r;
+    kx[t] = t % k;
     P.dy[t] = ky[t] - pad; P.dx[t] = kx[t] - pad;
   }
   P.Hg = y->h; P.Wg = y->w; P.oys = 1; P.oxs = 1; P.oy0 = 0; P.ox0 = 0;

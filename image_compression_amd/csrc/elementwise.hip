@@ -34,6 +34,38 @@ __global__ void nonneg_bwd_k(const float* p, const float* go, long long n, float
   }
 }
 
+// NonNegativeParam over up to NN_MAXT tensors in one launch (block c handles chunk c of the
+// concatenation; the per-element expressions are nonneg_fwd_k's / nonneg_bwd_k's, bitwise)
+constexpr int NN_MAXT = 16, NN_CHUNK = 2048;
+struct NonNegMulti {
+  const float* p[NN_MAXT];
+  float* out[NN_MAXT];
+  const float* go[NN_MAXT];
+  float* gi[NN_MAXT];
+  long long n[NN_MAXT];
+  float bound[NN_MAXT], ped[NN_MAXT];
+  int chunk_begin[NN_MAXT + 1];
+  int nt;
+};
+template <bool BWD>
+__global__ void __launch_bounds__(256) nonneg_multi_k(const NonNegMulti a) {
+  const int c = blockIdx.x;
+  int k = 0;
+  while (k + 1 < a.nt && c >= a.chunk_begin[k + 1]) ++k;
+  const long long base = (long long)(c - a.chunk_begin[k]) * NN_CHUNK;
+  const long long end = base + NN_CHUNK < a.n[k] ? base + NN_CHUNK : a.n[k];
+  for (long long i = base + threadIdx.x; i < end; i += blockDim.x) {
+    const float x = a.p[k][i];
+    const float v = fmaxf(x, a.bound[k]);
+    if (BWD) {
+      const float g = a.go[k][i] * v * 2.f;
+      a.gi[k][i] = (x >= a.bound[k] || g < 0.f) ? g : 0.f;
+    } else {
+      a.out[k][i] = v * v - a.ped[k];
+    }
+  }
+}
+
 __global__ void bound_fwd_k(const float* x, long long n, float b, int upper, float* y) {
   GRID_STRIDE(i, n) {
     const float v = x[i];
@@ -211,6 +243,33 @@ int ic_nonneg_fwd(const float* p, long long n, float bound, float ped, float* ou
 int ic_nonneg_bwd(const float* p, const float* gout, long long n, float bound, float* gin, void* stream) {
   hipLaunchKernelGGL(nonneg_bwd_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, gout, n, bound, gin);
   IC_CHECK_LAUNCH();
+  return IC_OK;
+}
+int ic_nonneg_multi(const ic_nonneg_tensor* ts, int ntensors, int backward, void* stream) {
+  if (ntensors < 0 || (ntensors > 0 && !ts)) return IC_ERR_ARG;
+  int cur = 0;
+  while (cur < ntensors) {
+    NonNegMulti a;
+    a.nt = 0;
+    int chunks = 0;
+    for (; cur < ntensors && a.nt < NN_MAXT; ++cur) {
+      const ic_nonneg_tensor& e = ts[cur];
+      if (e.n <= 0) continue;
+      if (!e.p || (backward ? (!e.gout || !e.gin) : !e.out)) return IC_ERR_ARG;
+      const int k = a.nt++;
+      a.p[k] = e.p; a.out[k] = e.out; a.go[k] = e.gout; a.gi[k] = e.gin;
+      a.n[k] = e.n; a.bound[k] = e.bound; a.ped[k] = e.pedestal;
+      a.chunk_begin[k] = chunks;
+      chunks += (int)((e.n + NN_CHUNK - 1) / NN_CHUNK);
+    }
+    if (a.nt == 0) continue;
+    a.chunk_begin[a.nt] = chunks;
+    if (backward)
+      hipLaunchKernelGGL(nonneg_multi_k<true>, dim3(chunks), dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(nonneg_multi_k<false>, dim3(chunks), dim3(256), 0, (hipStream_t)stream, a);
+    IC_CHECK_LAUNCH();
+  }
   return IC_OK;
 }
 int ic_bound_fwd(const float* x, long long n, float bound, int upper, float* y, void* stream) {

@@ -23,6 +23,9 @@
 // 64-channel-chunk kernel keeps the 128-row tiles: 0.378 vs 0.412 ms on g_a.2)
 #define IG_BF16_S 1
 #endif
+#ifndef IG_BF16_NARROW
+#define IG_BF16_NARROW 0  // 1: bf16 operands on the 32-channel-chunk kernel at 128-row tiles too
+#endif
 
 namespace {
 
@@ -966,7 +969,7 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
   const bool sq = d.a_op == AOP_SQUARE;
   switch (ig_kernel_kind(d)) {
     case IC_KERNEL_IG_SPLIT_BF16:
-      if constexpr (BN % 64 == 0 && BM == 64) {
+      if constexpr (BN % 64 == 0 && (BM == 64 || (IG_BF16_NARROW && BM == 128))) {
         if (sq) return IC_ERR_ARG;
         hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN, 1>), grid, dim3(256), 0, s, d);
         break;
@@ -980,9 +983,6 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
       }
       return IC_ERR_ARG;
     case IC_KERNEL_IG_SPLIT:
-      if constexpr (BN % 64 == 0 && BM == 128) {
-
-      }
       if constexpr (BN % 64 == 0) {
         hipLaunchKernelGGL((ig_kernel_x3s<BM, BN, WM, WN>), grid, dim3(64 * (BM / WM) * (BN / WN)), 0, s, d);
         break;
@@ -1004,7 +1004,9 @@ int ig_launch_t(const IgDesc& d, hipStream_t s) {
 
 // bf16 operands on the padded 64-channel-chunk kernel (ig_kernel_bf16) rather
 // than the swizzled 32-channel one (ig_kernel_x3s<..., 1>)
-static bool ig_bf16_wide(const IgDesc& d) { return d.bf16 && !(IG_BF16_S && d.bn % 64 == 0 && d.bm == 64); }
+static bool ig_bf16_wide(const IgDesc& d) {
+  return d.bf16 && !(IG_BF16_S && d.bn % 64 == 0 && (d.bm == 64 || (IG_BF16_NARROW && d.bm == 128)));
+}
 
 int ig_npad(int Cout) {
   if (Cout % 192 == 0) return Cout;

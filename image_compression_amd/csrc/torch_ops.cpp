@@ -335,6 +335,33 @@ Tensor nonneg_bwd(const Tensor& p, const Tensor& g, double bound) {
            "nonneg_bwd");
   return gi;
 }
+// NonNegativeParam of several tensors, one launch (ic_nonneg_multi)
+std::vector<Tensor> nonneg_multi_run(at::TensorList p, at::TensorList g, at::ArrayRef<double> bound,
+                                     at::ArrayRef<double> ped, bool bwd) {
+  TORCH_CHECK(p.size() == bound.size() && (bwd ? g.size() == p.size() : ped.size() == p.size()),
+              "nonneg_multi: one bound (and pedestal / gradient) per tensor");
+  std::vector<Tensor> outs;
+  std::vector<ic_nonneg_tensor> ts(p.size());
+  for (size_t i = 0; i < p.size(); ++i) {
+    check_dense(p[i], "param");
+    TORCH_CHECK(p[i].device() == p[0].device(), "nonneg_multi: tensors on one device");
+    if (bwd) check_same_layout(p[i], g[i], "gradient");
+    outs.push_back(like(p[i]));
+    ts[i] = ic_nonneg_tensor{p[i].data_ptr<float>(), bwd ? nullptr : outs[i].data_ptr<float>(),
+                             bwd ? g[i].data_ptr<float>() : nullptr, bwd ? outs[i].data_ptr<float>() : nullptr,
+                             (long long)p[i].numel(), (float)bound[i], bwd ? 0.f : (float)ped[i]};
+  }
+  if (p.empty()) return outs;
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p[0].device());
+  check_rc(ic_nonneg_multi(ts.data(), (int)ts.size(), bwd ? 1 : 0, stream_of(p[0])), "nonneg_multi");
+  return outs;
+}
+std::vector<Tensor> nonneg_multi_fwd(at::TensorList p, at::ArrayRef<double> bound, at::ArrayRef<double> ped) {
+  return nonneg_multi_run(p, {}, bound, ped, false);
+}
+std::vector<Tensor> nonneg_multi_bwd(at::TensorList p, at::TensorList g, at::ArrayRef<double> bound) {
+  return nonneg_multi_run(p, g, bound, {}, true);
+}
 Tensor bound_fwd(const Tensor& x, double bound, bool upper) {
   check_dense(x, "x");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
@@ -764,6 +791,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_meta(const Tensor& x, con
 Tensor like_meta1(const Tensor& x) { return at::empty_like(x, at::MemoryFormat::Preserve); }
 Tensor nonneg_fwd_meta(const Tensor& p, double, double) { return like_meta1(p); }
 Tensor nonneg_bwd_meta(const Tensor& p, const Tensor&, double) { return like_meta1(p); }
+std::vector<Tensor> nonneg_multi_fwd_meta(at::TensorList p, at::ArrayRef<double>, at::ArrayRef<double>) {
+  std::vector<Tensor> o;
+  for (const auto& t : p) o.push_back(like_meta1(t));
+  return o;
+}
+std::vector<Tensor> nonneg_multi_bwd_meta(at::TensorList p, at::TensorList, at::ArrayRef<double>) {
+  std::vector<Tensor> o;
+  for (const auto& t : p) o.push_back(like_meta1(t));
+  return o;
+}
 Tensor bound_fwd_meta(const Tensor& x, double, bool) { return like_meta1(x); }
 Tensor bound_bwd_meta(const Tensor& x, const Tensor&, double, bool) { return like_meta1(x); }
 Tensor unary_meta(const Tensor& x) { return like_meta1(x); }
@@ -850,6 +887,8 @@ TORCH_LIBRARY(imgcomp, m) {
         "(Tensor, Tensor, Tensor, Tensor)");
   m.def("nonneg_fwd(Tensor p, float bound, float pedestal) -> Tensor");
   m.def("nonneg_bwd(Tensor p, Tensor grad, float bound) -> Tensor");
+  m.def("nonneg_multi_fwd(Tensor[] p, float[] bound, float[] pedestal) -> Tensor[]");
+  m.def("nonneg_multi_bwd(Tensor[] p, Tensor[] grad, float[] bound) -> Tensor[]");
   m.def("bound_fwd(Tensor x, float bound, bool upper) -> Tensor");
   m.def("bound_bwd(Tensor x, Tensor grad, float bound, bool upper) -> Tensor");
   m.def("relu_fwd(Tensor x) -> Tensor");
@@ -898,6 +937,8 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("gdn_bwd_sum", gdn_bwd_sum);
   m.impl("nonneg_fwd", nonneg_fwd);
   m.impl("nonneg_bwd", nonneg_bwd);
+  m.impl("nonneg_multi_fwd", nonneg_multi_fwd);
+  m.impl("nonneg_multi_bwd", nonneg_multi_bwd);
   m.impl("bound_fwd", bound_fwd);
   m.impl("bound_bwd", bound_bwd);
   m.impl("relu_fwd", relu_fwd);
@@ -938,6 +979,8 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("gdn_bwd_sum", gdn_bwd_sum_meta);
   m.impl("nonneg_fwd", nonneg_fwd_meta);
   m.impl("nonneg_bwd", nonneg_bwd_meta);
+  m.impl("nonneg_multi_fwd", nonneg_multi_fwd_meta);
+  m.impl("nonneg_multi_bwd", nonneg_multi_bwd_meta);
   m.impl("bound_fwd", bound_fwd_meta);
   m.impl("bound_bwd", bound_bwd_meta);
   m.impl("relu_fwd", unary_meta);

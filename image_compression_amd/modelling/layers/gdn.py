@@ -26,6 +26,9 @@ class NonNegativeParam(nn.Module):
         self.param = nn.Parameter(torch.sqrt(torch.max(init_val + ped, ped)))
 
     def forward(self):
+        pre = self.__dict__.pop("_pre", None)  # this step's value, formed with its siblings' (see
+        if pre is not None:                    # Compressor2018: one NonNegMultiFn per transform)
+            return pre
         return nonneg_cached(self.param, float(self.bound), float(self.pedestal))
 
 

@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from ... import noise as _noise
-from ...functional import AbsFn, route_weight_gradients
+from ...functional import AbsFn, NonNegMultiFn, route_weight_gradients
 from ..blocks import (ENTROPY_MODEL_REGISTRY, AnalysisTransform, HyperpriorAnalysisTransform,
                       HyperpriorSynthesisTransform, SynthesisTransform)
 from ..layers import LowerBound, UpperBound
@@ -92,9 +92,26 @@ class Compressor2018(nn.Module):
         rest = [p for m in self.hyperprior_modules() for p in m.parameters() if id(p) not in ids]
         return [(wgrad_stream(device), convs), (side_stream(device), rest)]
 
+    def _reparameterise_gdn(self, x):
+        """Each main transform's GDN gamma / beta (NonNegativeParam) formed by one launch, their
+        gradients by one more (functional.NonNegMultiFn), instead of two launches per parameter;
+        every NonNegativeParam returns the value formed here at its next call.  Only with autograd
+        on a device tensor (the eval weight cache keeps its own values)."""
+        from ..layers.gdn import NonNegativeParam
+        for blk in (self.analysis_transform, self.synthesis_transform):
+            mods = [m for m in blk.modules() if isinstance(m, NonNegativeParam)]
+            for m in mods:
+                m.__dict__.pop("_pre", None)
+            if mods and x.is_cuda and torch.is_grad_enabled():
+                vals = NonNegMultiFn.apply([float(m.bound) for m in mods], [float(m.pedestal) for m in mods],
+                                           *[m.param for m in mods])
+                for m, v in zip(mods, vals):
+                    m.__dict__["_pre"] = v
+
     def forward(self, x):
         if self.training:
             _noise.begin_step(x.device)  # fresh Philox counters for this step
+        self._reparameterise_gdn(x)
         N, _, H, W = x.shape
         num_pixels = N * H * W
         y = self.analysis_transform(x)

@@ -215,6 +215,20 @@ int ic_conv_plan(int op, const ic_act* a, const ic_act* b, int k, int stride, in
 /* NonNegativeParam: v = max(p, bound); out = v*v - ped */
 int ic_nonneg_fwd(const float* p, long long n, float bound, float ped, float* out, void* stream);
 int ic_nonneg_bwd(const float* p, const float* gout, long long n, float bound, float* gin, void* stream);
+/* NonNegativeParam of several tensors in one launch (a training step's GDN gamma / beta:
+ * reference gdn.py:59-62, called once per GDN layer): per tensor, backward = 0 -> out = max(p,
+ * bound)^2 - pedestal; backward = 1 -> gin = the gradient of ic_nonneg_bwd given gout.  Bitwise the
+ * per-tensor entry points. */
+typedef struct ic_nonneg_tensor {
+  const float* p;
+  float* out;          /* forward output (unused in the backward) */
+  const float* gout;   /* backward: dL/dout */
+  float* gin;          /* backward: dL/dp */
+  long long n;
+  float bound;
+  float pedestal;
+} ic_nonneg_tensor;
+int ic_nonneg_multi(const ic_nonneg_tensor* tensors, int ntensors, int backward, void* stream);
 /* LowerBound (upper=0): max(x,b); UpperBound (upper=1): min(x,b) — with the reference's
  * pass-through gradients */
 int ic_bound_fwd(const float* x, long long n, float bound, int upper, float* y, void* stream);

@@ -237,6 +237,11 @@ def _meta_cases():
     return {
         "nonneg_fwd": (lambda o: o.nonneg_fwd(_meta(192, 192), 0.0, 2 ** -36), [(192, 192)]),
         "nonneg_bwd": (lambda o: o.nonneg_bwd(_meta(192), _meta(192), 0.0), [(192,)]),
+        "nonneg_multi_fwd": (lambda o: tuple(o.nonneg_multi_fwd([_meta(192, 192), _meta(192)], [0.0, 1e-3],
+                                                                 [2 ** -36, 2 ** -36])), [(192, 192), (192,)]),
+        "nonneg_multi_bwd": (lambda o: tuple(o.nonneg_multi_bwd([_meta(192, 192), _meta(192)],
+                                                                 [_meta(192, 192), _meta(192)], [0.0, 1e-3])),
+                             [(192, 192), (192,)]),
         "bound_fwd": (lambda o: o.bound_fwd(img, 1.0, True), [img.shape]),
         "bound_bwd": (lambda o: o.bound_bwd(img, img, 0.0, False), [img.shape]),
         "relu_fwd": (lambda o: o.relu_fwd(x), [s]),
