@@ -66,7 +66,8 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
   if (!need && (!split || x->c == 192) && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
       ((uintptr_t)gamma & 15) == 0) {
-    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s, split ? 1 : 0);
+    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s,
+                         (math & IC_MATH_BF16) && split && x->c == 192 ? 2 : split ? 1 : 0);
   }
   IgDesc d = {};
   gemm1x1(d, x, y);
@@ -178,7 +179,10 @@ int gdn_plan(int bwd, const ic_act* x, int math) {
   if (!bwd) {
     const bool fsplit = split && x->c % 32 == 0 && x->sc == 1 && x->c >= 64;
     if ((!fsplit || x->c == 192) && fused) {
-      plan_report(fsplit ? IC_KERNEL_GDN_FUSED_SPLIT : IC_KERNEL_GDN_FUSED, fsplit ? 32 : 16, x->c, 1, 0, 0, -1);
+      plan_report(fsplit && (math & IC_MATH_BF16) ? IC_KERNEL_GDN_FUSED_BF16
+                  : fsplit                         ? IC_KERNEL_GDN_FUSED_SPLIT
+                                                   : IC_KERNEL_GDN_FUSED,
+                  fsplit ? 32 : 16, x->c, 1, 0, 0, -1);
       return IC_OK;
     }
   } else if (fused) {

@@ -252,20 +252,24 @@ __global__ void __launch_bounds__(256, 2)
 // y and norm leave straight from the MFMA result registers (each 16-lane group
 // writes 64 contiguous bytes of a pixel row; the 12 waves fill the row): no norm
 // staging image and no copy-out pass.
-template <int C>
+//
+// NP = 1 (IC_MATH_BF16, config C3): the same kernel on bf16 operands -- Gamma and x^2 rounded to
+// nearest even, one plane each, one product, fp32 accumulation.
+template <int C, int NP = 3>
 __global__ void __launch_bounds__(768, 1)
     gdn_fwd_x3s_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                        const float* __restrict__ beta, int inverse, float* __restrict__ y,
                        float* __restrict__ norm, uint32_t P) {
   static_assert(C == 192, "12 waves x 16 channels");
+  static_assert(NP == 3 || NP == 1, "split (3 planes) or bf16 (1 plane)");
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   constexpr int BM = 32, NT = 768;
   constexpr int TILE = BM * C;
   constexpr int KU = C / 32;
   constexpr int QS = BM * C / 4 / NT;  // float4 per thread in staging and in the split pass
-  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];   // three x buffers
-  __shared__ __attribute__((aligned(16))) __bf16 sq[6 * TILE];  // two sets of three x^2 planes
+  __shared__ __attribute__((aligned(16))) float lds[3 * TILE];        // three x buffers
+  __shared__ __attribute__((aligned(16))) __bf16 sq[2 * NP * TILE];  // two sets of NP x^2 planes
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -273,16 +277,21 @@ __global__ void __launch_bounds__(768, 1)
   const uint32_t ntiles = (P + BM - 1) / BM;
   const uint32_t G = gridDim.x;
 
-  b8 bg[3][KU];
+  b8 bg[NP][KU];
 #pragma unroll
   for (int u = 0; u < KU; ++u) {
     const floatx4v g0 = *(const floatx4v*)(gamma + (size_t)n * C + 32 * u + 8 * lg);
     const floatx4v g1 = *(const floatx4v*)(gamma + (size_t)n * C + 32 * u + 8 * lg + 4);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      __bf16 hh, mm, ll;
-      split3_bf16(e < 4 ? g0[e] : g1[e - 4], hh, mm, ll);
-      bg[0][u][e] = hh; bg[1][u][e] = mm; bg[2][u][e] = ll;
+      const float gv = e < 4 ? g0[e] : g1[e - 4];
+      if constexpr (NP == 1) {
+        bg[0][u][e] = (__bf16)gv;  // round to nearest even
+      } else {
+        __bf16 hh, mm, ll;
+        split3_bf16(gv, hh, mm, ll);
+        bg[0][u][e] = hh; bg[NP - 2][u][e] = mm; bg[NP - 1][u][e] = ll;
+      }
     }
   }
   float bet = beta[n];
@@ -318,12 +327,18 @@ __global__ void __launch_bounds__(768, 1)
       const int pos = tid + NT * q;
       const int m = srow[q], lc = scol[q] >> 2;
       const floatx4v v = *(const floatx4v*)(xs + pos * 4);
-      b4 vh, vm, vl;
-      split3_bf16x4(v * v, vh, vm, vl);
       const int off = m * C + 8 * ((lc >> 1) ^ ((m >> 1) & 7)) + 4 * (lc & 1);
-      *(b4*)(sb + off) = vh;
-      *(b4*)(sb + TILE + off) = vm;
-      *(b4*)(sb + 2 * TILE + off) = vl;
+      if constexpr (NP == 1) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        const floatx4v v2 = v * v;
+        *(b4*)(sb + off) = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v2[0], v2[1]), ic_cvt_pk_bf16(v2[2], v2[3])});
+      } else {
+        b4 vh, vm, vl;
+        split3_bf16x4(v * v, vh, vm, vl);
+        *(b4*)(sb + off) = vh;
+        *(b4*)(sb + TILE + off) = vm;
+        *(b4*)(sb + 2 * TILE + off) = vl;
+      }
     }
   };
 
@@ -348,9 +363,9 @@ __global__ void __launch_bounds__(768, 1)
     __builtin_amdgcn_s_barrier();
     const int b1 = bx == 2 ? 0 : bx + 1, b2 = b1 == 2 ? 0 : b1 + 1;
     load(tile + 3 * G < ntiles ? tile + 3 * G : tile, ld);
-    if (tile + G < ntiles) split_pass(lds + b1 * TILE, sq + (sb ^ 1) * 3 * TILE);
+    if (tile + G < ntiles) split_pass(lds + b1 * TILE, sq + (sb ^ 1) * NP * TILE);
     const float* xs = lds + bx * TILE;
-    const __bf16* sp = sq + sb * 3 * TILE;
+    const __bf16* sp = sq + sb * NP * TILE;
     floatx4v acc[BM / 16];
 #pragma unroll
     for (int mt = 0; mt < BM / 16; ++mt) {
@@ -359,13 +374,17 @@ __global__ void __launch_bounds__(768, 1)
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         const int ch = 8 * ((4 * u + lg) ^ fsw);
-        const b8 a0 = *(const b8*)(ar + ch), a1 = *(const b8*)(ar + TILE + ch), a2 = *(const b8*)(ar + 2 * TILE + ch);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bg[0][u], acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[1][u], acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[2][u], acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[0][u], acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[1][u], acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[0][u], acc[mt], 0, 0, 0);
+        if constexpr (NP == 1) {
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const b8*)(ar + ch), bg[0][u], acc[mt], 0, 0, 0);
+        } else {
+          const b8 a0 = *(const b8*)(ar + ch), a1 = *(const b8*)(ar + TILE + ch), a2 = *(const b8*)(ar + 2 * TILE + ch);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bg[0][u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[1][u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[2][u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bg[0][u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[1][u], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bg[0][u], acc[mt], 0, 0, 0);
+        }
       }
     }
     // epilogue (C/D map: col n = li, row m = 16mt + 4g + r) straight to y and norm; rows past P
@@ -881,12 +900,16 @@ bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long
 
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
                   long long P, hipStream_t s, int split) {
-  if (split && C == 192) {
+  if (split && C == 192) {  // split: 1 = fp32 by the exact split, 2 = bf16 operands (config C3)
     const long long ntiles = (P + 31) / 32;
     const long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
     if (grid < 1) return IC_OK;
-    hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse, y,
-                       norm, (uint32_t)P);
+    if (split == 2)
+      hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse,
+                         y, norm, (uint32_t)P);
+    else
+      hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse, y,
+                         norm, (uint32_t)P);
     IC_CHECK_LAUNCH();
     return IC_OK;
   }

@@ -28,10 +28,11 @@ def set_compute_dtype(model, dtype):
     transforms (1.3 % of the FLOPs, but they shape the rate term's gradients)
     run in "fp32_split" arithmetic there.  GDN,
     the entropy models and the 3-channel image edges compute in fp32 in every
-    mode, except that "fp32_split" and "bf16" run GDN (C = 192) in split
-    arithmetic too: the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at
-    128^2) and the fused backward's dgamma GEMM (GDN.math = 2: 4 % faster);
-    A/B in one process, tools/gdn_ab.py."""
+    mode, except that "fp32_split" runs GDN (C = 192) in split arithmetic too:
+    the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at 128^2) and the fused
+    backward's dgamma GEMM (GDN.math = 2: 4 % faster; A/B in one process,
+    tools/gdn_ab.py), and "bf16" runs both of the backward's contractions and the
+    forward's Gamma x^2 on bf16 operands (C = 192)."""
     from ...functional import MATH
     from ..layers.conv import Conv2d, ConvTranspose2d
     from ..layers.gdn import GDN
@@ -50,7 +51,8 @@ def set_compute_dtype(model, dtype):
             # the fused backward's dgamma GEMM in split arithmetic; bf16: both of its GEMMs on
             # bf16 operands (C = 192)
             m.math = split | (MATH["bf16"] if dtype == "bf16" else 0)
-            m.math_fwd = split  # the fused forward (C = 192) in split arithmetic
+            # the fused forward (C = 192) in split arithmetic; bf16: its Gamma x^2 GEMM on bf16 operands
+            m.math_fwd = split | (MATH["bf16"] if dtype == "bf16" else 0)
     for names, flag in ((main, flags[0]), (hyper, flags[1])):
         for name in names:
             sub = getattr(model, name, None)

@@ -78,30 +78,32 @@ def nonneg(param, minimum=0.0, offset=2.0 ** -18):
 
 
 def gdn(x, gamma_param, beta_param, inverse=False, relu=False,
-        beta_min=1e-6, offset=2.0 ** -18, bf16_bwd=False):
+        beta_min=1e-6, offset=2.0 ** -18, bf16_bwd=False, bf16_fwd=False):
     """modelling/layers/gdn.py:79-88: y = x / sqrt(conv1x1(x^2, gamma) + beta)
     (x * sqrt(...) when inverse).  bf16_bwd: the backward's two contractions take
-    bf16-rounded operands (_GDNBwdRounded; config C3 emulation, forward GDN only)."""
+    bf16-rounded operands (_GDNBwdRounded; config C3 emulation, forward GDN only);
+    bf16_fwd: the forward's gamma x^2 takes bf16-rounded gamma and x^2 (C3 emulation)."""
     if relu:
         x = F.relu(x)
     gamma = nonneg(gamma_param, 0.0, offset)
     beta = nonneg(beta_param, beta_min, offset)
-    if bf16_bwd and not inverse:
-        return _GDNBwdRounded.apply(x, gamma, beta)
+    if (bf16_bwd or bf16_fwd) and not inverse:
+        return _GDNBwdRounded.apply(x, gamma, beta, bool(bf16_fwd), bool(bf16_bwd))
     norm = torch.sqrt(F.conv2d(x * x, gamma, beta))
     return x * norm if inverse else x / norm
 
 
 class _GDNBwdRounded(torch.autograd.Function):
-    """y = x * (beta + gamma x^2)^-1/2 with the backward's contractions on bf16-rounded operands:
-    with v = beta + gamma x^2 and q = dL/dv = -1/2 dy x v^-3/2,
-    dx = dy v^-1/2 + 2 x (rnd(q) rnd(gamma)), dgamma = rnd(q)^T rnd(x^2), dbeta = sum q.
-    Not the reference's arithmetic: the emulation of config C3's bf16-operand GDN backward
-    (csrc/gdn_fused.hip, BF); the forward is exact."""
+    """y = x * v^-1/2, v = beta + gamma x^2, with the contractions on bf16-rounded operands where
+    flagged: forward (rf) v = beta + rnd(gamma) rnd(x^2); backward (rb), with q = dL/dv =
+    -1/2 dy x v^-3/2, dx = dy v^-1/2 + 2 x (rnd(q) rnd(gamma)), dgamma = rnd(q)^T rnd(x^2),
+    dbeta = sum q (exact operands where not flagged).  Not the reference's arithmetic: the emulation
+    of config C3's bf16-operand GDN (csrc/gdn_fused.hip, gdn_fwd_x3s_kernel<192, 1> and BF)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta):
-        v = F.conv2d(x * x, gamma, beta)
+    def forward(ctx, x, gamma, beta, rf=False, rb=True):
+        v = F.conv2d(_rnd(x * x), _rnd(gamma), beta) if rf else F.conv2d(x * x, gamma, beta)
+        ctx.rb = rb
         ctx.save_for_backward(x, gamma, v)
         return x / torch.sqrt(v)
 
@@ -110,13 +112,14 @@ class _GDNBwdRounded(torch.autograd.Function):
         x, gamma, v = ctx.saved_tensors
         rs = v.rsqrt()
         q = -0.5 * dy * x * rs * rs * rs
-        g2 = _rnd(gamma.reshape(gamma.shape[0], gamma.shape[1]))
-        qr = _rnd(q)
+        r = _rnd if ctx.rb else (lambda t: t)
+        g2 = r(gamma.reshape(gamma.shape[0], gamma.shape[1]))
+        qr = r(q)
         dxg = torch.einsum("bnhw,nk->bkhw", qr, g2)
         dx = dy * rs + 2.0 * x * dxg
-        dgamma = torch.einsum("bnhw,bkhw->nk", qr, _rnd(x * x)).reshape(gamma.shape)
+        dgamma = torch.einsum("bnhw,bkhw->nk", qr, r(x * x)).reshape(gamma.shape)
         dbeta = q.sum((0, 2, 3))
-        return dx, dgamma, dbeta
+        return dx, dgamma, dbeta, None, None
 
 
 def gdn_init(C, gamma_init=0.1, offset=2.0 ** -18):
@@ -193,7 +196,7 @@ class _ConvRounded(torch.autograd.Function):
 
 def _conv(x, w, b, stride, pad, name, bf16, transposed=False, opad=0):
     """F.conv2d / F.conv_transpose2d; with `bf16` (a dict: weight name -> (fwd, dgrad, wgrad)
-    flags, and GDN gamma-parameter name -> True for a bf16 backward) the GEMMs flagged for this
+    flags, and GDN gamma-parameter name -> (forward, backward) flags) the GEMMs flagged for this
     layer take bf16-rounded operands (_ConvRounded)."""
     flags = bf16.get(name) if bf16 else None
     if flags and any(flags):
@@ -212,8 +215,9 @@ def analysis(P, x, strides=(2, 2, 2, 2), k=5, prefix="analysis_transform.layers.
         name = f"{prefix}{2*i}.weight"
         x = _conv(x, P[name], P[f"{prefix}{2*i}.bias"], s, k // 2, name, bf16)
         if i < n - 1:
+            gf = bf16.get(f"{prefix}{2*i+1}.gamma.param") if bf16 else None
             x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"],
-                    bf16_bwd=bool(bf16 and bf16.get(f"{prefix}{2*i+1}.gamma.param")))
+                    bf16_bwd=bool(gf and gf[1]), bf16_fwd=bool(gf and gf[0]))
     return x
 
 
@@ -226,8 +230,9 @@ def synthesis(P, x, strides=(2, 2, 2, 2), k=5, prefix="synthesis_transform.layer
         name = f"{prefix}{2*i}.weight"
         x = _conv(x, P[name], P[f"{prefix}{2*i}.bias"], s, k // 2, name, bf16, transposed=True, opad=s - 1)
         if i < n - 1:
+            gf = bf16.get(f"{prefix}{2*i+1}.gamma.param") if bf16 else None
             x = gdn(x, P[f"{prefix}{2*i+1}.gamma.param"], P[f"{prefix}{2*i+1}.beta.param"],
-                    bf16_bwd=bool(bf16 and bf16.get(f"{prefix}{2*i+1}.gamma.param")))
+                    bf16_bwd=bool(gf and gf[1]), bf16_fwd=bool(gf and gf[0]))
     return x
 
 

@@ -155,11 +155,11 @@ def c3_bf16_flags(n, size, latent):
         f = (cin % 64 == 0 and cout > 4, cout % 64 == 0, cout > 4 and wg_ok(cin, cout, wi, n * wi * wi))
         flags[f"synthesis_transform.layers.{2 * i}.weight"] = f
         launches += sum(f)
-    # every GDN (C = 192, NHWC-dense: the fused kernel) has a bf16 backward
+    # every GDN (C = 192, NHWC-dense: the fused kernels) has a bf16 forward and backward
     for t in ("analysis_transform", "synthesis_transform"):
         for i in range(3):
-            flags[f"{t}.layers.{2 * i + 1}.gamma.param"] = True
-            launches += 1
+            flags[f"{t}.layers.{2 * i + 1}.gamma.param"] = (True, True)
+            launches += 2
     return flags, launches
 
 
@@ -210,7 +210,8 @@ def c3_check(model, params, x, uz, uy, xt, losses, masks, log, lam, latent, laye
             ref = ref_cpu._conv(a, P[nm + ".weight"], P[nm + ".bias"], 2, 2, nm + ".weight", flags, transposed=tr,
                                 opad=1 if tr else 0)
         else:
-            ref = ref_cpu.gdn(a, P[nm + ".gamma.param"], P[nm + ".beta.param"])
+            ref = ref_cpu.gdn(a, P[nm + ".gamma.param"], P[nm + ".beta.param"],
+                              bf16_fwd=bool(flags[nm + ".gamma.param"][0]))
         e = rel_err(b, ref)
         assert e < 1e-5, (nm, kind, e)
     ctl_x, ctl_e = {"masks": masks}, {"masks": masks}

@@ -166,3 +166,32 @@ def test_gdn_bwd_bf16(n, h, w, inverse):
             assert e2 < 1e-4, (nm, e2)  # q rounds from fp32 here, from fp64 there: rare neighbour flips
         print(msg)
     assert rel_err(got[2], ref[False][2]) < 1e-5
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 16, 16), (3, 7, 5), (4, 33, 31)])
+def test_gdn_fwd_bf16(n, h, w):
+    """GDN forward with IC_MATH_BF16 (gdn_fwd_x3s_kernel<192, 1>): Gamma x^2 on bf16 operands (one
+    plane, one product, fp32 accumulation).  Against fp64: bf16-level error; against the oracle's
+    emulation of those operands: fp32-class (x^2 rounds from fp32 here, from fp64 there)."""
+    from image_compression_amd import _lib
+    from image_compression_amd.modelling.layers import GDN
+    from oracle import ref_cpu
+    torch.manual_seed(0)
+    m = GDN(192)
+    with torch.no_grad():
+        m.gamma.param.add_(torch.rand_like(m.gamma.param) * 0.05)
+        m.beta.param.add_(torch.rand_like(m.beta.param) * 0.1)
+    x = _r(n, 192, h, w, seed=14)
+    gp, bp = m.gamma.param.detach().double(), m.beta.param.detach().double()
+    exact = ref_cpu.gdn(x.double(), gp, bp)
+    emul = ref_cpu.gdn(x.double(), gp, bp, bf16_fwd=True)
+    md = m.to(DEV)
+    md.math_fwd = 3   # split | bf16
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    assert _lib.plan("gdn_fwd", xd, None, math=3)["kernel"] == "gdn_fused_bf16"
+    with torch.no_grad():
+        y = md(xd).cpu()
+    e, e2 = rel_err(y, exact), rel_err(y, emul)
+    print(f"gdn fwd bf16: vs fp64 {e:.2e}, vs fp64 of the bf16 operands {e2:.2e}")
+    assert e < 1e-2 and e2 < 1e-4, (e, e2)
+    assert e2 < e / 4  # the kernel computes what the config says, not plain fp32
