@@ -72,11 +72,11 @@ def test_concurrent_steps_exact_and_factorized_backward_recomputes():
                 for j, (a, b) in enumerate(zip(out, grads)):
                     assert torch.equal(a, b), ("factorized backward differs from its recompute", i, j)
             assert len(wsnaps) == 6, len(wsnaps)   # h_a's three convs and h_s's three
-            for x, gy, w, conf, has_b, dw, db in wsnaps:
+            for xs, gy, w, conf, has_b, dw, db in wsnaps:
                 transposed, stride, padding, act, math = conf
                 assert not act
                 fn = ops.conv_transpose2d_wgrad if transposed else ops.conv2d_wgrad
-                dw2, db2 = fn(x, gy, w, stride, padding, has_b, math)
+                dw2, db2 = fn(xs, gy, w, stride, padding, has_b, math)
                 torch.cuda.synchronize()
                 assert torch.equal(dw, dw2), ("hyperprior weight gradient differs from its recompute", i, conf)
                 assert db is None or torch.equal(db, db2), ("hyperprior bias gradient differs", i, conf)

@@ -15,4 +15,8 @@ timeout -k 10 400 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_
 cat gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAIL; tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
+# the dominant kernel's launches inside bench's timed steps only (bench.py IMGCOMP_ROCTX_DOMINANT: roctx
+# resume / pause around the layer the roofline times), so the stats average is the launches `roofline` reports
+IMGCOMP_ROCTX_DOMINANT=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --selected-regions -d $R/gpurun_out/dom_$TAG -o dom --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/dom_$TAG.log 2>&1 || { echo DOM PROF FAIL; tail -20 $R/gpurun_out/dom_$TAG.log; exit 1; }
+grep -h "ig_kernel_x3d\|Name" $(find $R/gpurun_out/dom_$TAG -name "*kernel_stats.csv") | head -3
 echo DONE
