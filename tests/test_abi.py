@@ -174,6 +174,8 @@ def test_plan_query_c2_instances():
     assert _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 2)["kernel"] == "edge_conv"
     assert _lib.plan("conv_transpose2d_fwd", x, img, 5, 2, 2, 2)["kernel"] == "tconv_few_rows"
     assert _lib.plan("gdn_fwd", x, math=2)["kernel"] == "gdn_fused_split"
+    assert _lib.plan("gdn_fwd", x, math=3)["kernel"] == "gdn_fused_bf16"   # C3: split | bf16
+    assert _lib.plan("gdn_bwd", x, math=3)["kernel"] == "gdn_fused_bf16"
     assert _lib.plan("gdn_bwd", x, math=0)["kernel"] == "gdn_fused"
 
 
