@@ -155,15 +155,6 @@ class LiveLaunchTimer:
         self.on = False
         self.pairs = []
         self._e0 = None
-        # IMGCOMP_ROCTX_DOMINANT=1 under `rocprofv3 --selected-regions`: the profiler records only
-        # these launches (roctxProfilerResume / Pause around the module's forward inside the timed
-        # steps), so the committed --stats summary averages exactly the launches `roofline` times
-        self._roctx = None
-        if os.environ.get("IMGCOMP_ROCTX_DOMINANT") == "1":
-            import ctypes
-            self._roctx = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
-            for fn in (self._roctx.roctxProfilerResume, self._roctx.roctxProfilerPause):
-                fn.argtypes = [ctypes.c_uint64]  # roctx_thread_id_t; 0 = every thread
         module.register_forward_pre_hook(self._pre)
         module.register_forward_hook(self._post)
 
@@ -174,16 +165,12 @@ class LiveLaunchTimer:
 
     def _pre(self, mod, inp):
         if self.on:
-            if self._roctx is not None:
-                self._roctx.roctxProfilerResume(0)
             self._e0 = self._event()
 
     def _post(self, mod, inp, out):
         if self.on and self._e0 is not None:
             self.pairs.append((self._e0, self._event()))
             self._e0 = None
-            if self._roctx is not None:
-                self._roctx.roctxProfilerPause(0)
 
     def ms(self):
         """Average launch duration (call after synchronize), or None."""

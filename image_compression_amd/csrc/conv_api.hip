@@ -11,7 +11,7 @@
 #include "gemm.h"
 
 #ifndef TAP_PARITY_ORDER
-#define TAP_PARITY_ORDER 0  // 1: stride-2 direct convs walk even kernel rows first, then odd (conv_impl)
+#define TAP_PARITY_ORDER 1  // stride-2 direct convs walk even kernel rows first, then odd (conv_impl); 0: row order
 #endif
 
 thread_local ic_plan* g_plan_sink = nullptr;
@@ -180,8 +180,8 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   for (int t = 0; t < P.T; ++t) {
     // TAP_PARITY_ORDER: kernel rows 0, 2, 4, 1, 3 (k = 5).  Tap row ky reads input rows 2y + ky - pad,
     // so even and odd kernel rows read disjoint rows: taken parity by parity, the input rows a
-    // channel chunk's taps read stay in the XCD's L2 across those taps (r05a: no gain on the
-    // split kernels, which are not bound by those bytes)
+    // channel chunk's taps read stay in the XCD's L2 across those taps.  r05e, PMC FETCH per g_a.2
+    // fwd launch: ig_kernel_x3d 0.86 -> 0.58 GB, ig_kernel_bf16 1.65 -> 1.09 GB; time equal / -2.5 %
     const int r = t / k, ne = (k + 1) / 2;
     ky[t] = (stride == 2 && TAP_PARITY_ORDER) ? (r < ne ? 2 * r : 2 * (r - ne) + 1) : r;
     kx[t] = t % k;

@@ -3,9 +3,9 @@ weight gradients on a stream of their own, beside the synthesis transform's MFMA
 serial reference step, bitwise, with every factorized-backward and hyperprior weight-gradient
 launch recomputed on its own inputs on an idle GPU.  Guards the fault found in round 3: with
 packed-fp32 VALU instructions (v_pk_*_f32) the factorized backward (csrc/entropy.hip fact_bwd_k)
-returned a wrong w1 / w2 gradient element in 1 of 120 concurrent steps (47 of 120 with an LDS-only
-reduction), never in serial steps; the VALU-only kernels are now built without them (Makefile
-NOPK_SRCS) and 440 concurrent steps came out exact (tools/race_probe.py).  GPU only."""
+returned wrong w1 / w2 gradient elements in concurrent steps only (1 of 120; 53 of 80 with an
+LDS-only reduction), never without those instructions; every source is now built without them
+(csrc/Makefile NOPK, tests/test_isa_scan.py) -- DESIGN.md 10a.  GPU only."""
 import pytest
 import torch
 
@@ -36,7 +36,7 @@ def test_concurrent_steps_exact_and_factorized_backward_recomputes():
         x, w = ctx.saved_tensors
         res = orig_wg(ctx, gz)
         # stream-ordered clones on the weight-gradient stream (the backward's own stream)
-        wsnaps.append((x.clone(), IF._cl(gz).clone(), w, ctx.conf, ctx.has_b, res[1].clone(),
+        wsnaps.append((x.clone(), IF._cl(gz).clone(), w.detach(), ctx.conf, ctx.has_b, res[1].clone(),
                        None if res[2] is None else res[2].clone()))
         return res
 
@@ -65,21 +65,27 @@ def test_concurrent_steps_exact_and_factorized_backward_recomputes():
     IF._ConvWGradFn.backward = staticmethod(wrapped_wg)
     try:
         for i in range(30):
-            r = step(True)
-            for q, prm, gq, gp, C, out in snaps:
-                dz, grads = ops.factorized_bwd(q, C, prm, gq, gp)
-                torch.cuda.synchronize()
-                for j, (a, b) in enumerate(zip(out, grads)):
-                    assert torch.equal(a, b), ("factorized backward differs from its recompute", i, j)
-            assert len(wsnaps) == 6, len(wsnaps)   # h_a's three convs and h_s's three
-            for xs, gy, w, conf, has_b, dw, db in wsnaps:
-                transposed, stride, padding, act, math = conf
-                assert not act
-                fn = ops.conv_transpose2d_wgrad if transposed else ops.conv2d_wgrad
-                dw2, db2 = fn(xs, gy, w, stride, padding, has_b, math)
-                torch.cuda.synchronize()
-                assert torch.equal(dw, dw2), ("hyperprior weight gradient differs from its recompute", i, conf)
-                assert db is None or torch.equal(db, db2), ("hyperprior bias gradient differs", i, conf)
+            try:
+                r = step(True)
+            except UserWarning as e:   # conftest makes the AccumulateGrad stream warning an error
+                raise AssertionError(f"concurrent step {i}: {str(e)[:120]}") from e
+            # recomputes without autograd: a call on the parameter itself in grad mode would hang a
+            # graph node (and the parameter's AccumulateGrad, made on this stream) on its output
+            with torch.no_grad():
+                for q, prm, gq, gp, C, out in snaps:
+                    dz, grads = ops.factorized_bwd(q, C, prm, gq, gp)
+                    torch.cuda.synchronize()
+                    for j, (a, b) in enumerate(zip(out, grads)):
+                        assert torch.equal(a, b), ("factorized backward differs from its recompute", i, j)
+                assert len(wsnaps) == 6, len(wsnaps)   # h_a's three convs and h_s's three
+                for xs, gy, w, conf, has_b, dw, db in wsnaps:
+                    transposed, stride, padding, act, math = conf
+                    assert not act
+                    fn = ops.conv_transpose2d_wgrad if transposed else ops.conv2d_wgrad
+                    dw2, db2 = fn(xs, gy, w, stride, padding, has_b, math)
+                    torch.cuda.synchronize()
+                    assert torch.equal(dw, dw2), ("hyperprior weight gradient differs from its recompute", i, conf)
+                    assert db is None or torch.equal(db, db2), ("hyperprior bias gradient differs", i, conf)
             snaps.clear()
             wsnaps.clear()
             for k in ref:

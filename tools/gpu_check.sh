@@ -14,9 +14,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 400 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo BENCH FAIL; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAIL; tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
-# the dominant kernel's launches inside bench's timed steps only (bench.py IMGCOMP_ROCTX_DOMINANT: roctx
-# resume / pause around the layer the roofline times), so the stats average is the launches `roofline` reports
-IMGCOMP_ROCTX_DOMINANT=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --selected-regions -d $R/gpurun_out/dom_$TAG -o dom --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/dom_$TAG.log 2>&1 || { echo DOM PROF FAIL; tail -20 $R/gpurun_out/dom_$TAG.log; exit 1; }
-grep -h "ig_kernel_x3d\|Name" $(find $R/gpurun_out/dom_$TAG -name "*kernel_stats.csv") | head -3
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAIL; tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
+# the dominant kernel's launches the roofline times live (g_a.2 fwd: the first main-queue ig_kernel_x3d of each
+# step) from the same trace, to set beside bench's live figure
+python3 $R/tools/trace_timeline.py $(find $R/gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1) --first ig_kernel_x3d | head -2
 echo DONE

@@ -33,6 +33,11 @@ def main(src, specs):
         for name in fetch:
             if key not in name:
                 continue
+            if alg == 0:   # launches of several shapes: every launch's bytes, in launch order
+                ws = write.get(name, [0.0] * len(fetch[name]))
+                print(f"{name[:70]}: per-launch traffic MB " + " ".join(
+                    f"{(2 * f + w) * 1024 / 1e6:.1f}" for f, w in zip(fetch[name], ws)))
+                continue
             fb = 2 * statistics.median(fetch[name]) * 1024
             wb = statistics.median(write.get(name, [0.0])) * 1024
             st = next((v for k, v in stats.items() if k == name), None)

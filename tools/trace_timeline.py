@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--step", type=int, default=-2, help="which step (python index over the delimited steps)")
     ap.add_argument("--list", action="store_true", help="print every kernel of the step")
     ap.add_argument("--gap-us", type=float, default=8.0)
+    ap.add_argument("--first", default=None, help="report the first main-queue launch of this kernel in every "
+                    "delimited step (ig_kernel_x3d: g_a.2 fwd, the launch bench.py's roofline times live)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     for r in rows:
@@ -37,6 +39,16 @@ def main():
     steps = [(marks[i], marks[i + 1]) for i in range(len(marks) - 1)]
     print(f"{len(rows)} kernels, {len(steps)} delimited steps; step spans (ms): "
           + " ".join(f"{(rows[e]['t0'] - rows[b]['t0']) / 1e3:.3f}" for b, e in steps))
+    if a.first:
+        ds = []
+        for b, e in steps:
+            mq = rows[b]["q"]
+            k = next((r for r in rows[b:e] if r["q"] == mq and a.first in r["n"]), None)
+            if k is not None:
+                ds.append(k["t1"] - k["t0"])
+        if ds:
+            print(f"first main-queue {a.first} per step: {len(ds)} launches, mean {sum(ds) / len(ds) / 1e3:.4f} ms, "
+                  f"min {min(ds) / 1e3:.4f}, max {max(ds) / 1e3:.4f} ms")
     b, e = steps[a.step]
     st = rows[b:e]
     t_start, t_end = st[0]["t0"], rows[e]["t0"]
