@@ -52,7 +52,9 @@ def _st():
 
 def _key(device):
     d = torch.device(device)
-    return (d.type, d.index if d.index is not None else torch.cuda.current_device())
+    if d.index is None:
+        return (d.type, torch.cuda.current_device() if d.type == "cuda" else 0)
+    return (d.type, d.index)
 
 
 _MASK62 = (1 << 62) - 1

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the C2 training step (batch 32, 256^2, fp32_split) with and without the
-hyperprior side stream (Compressor2018.concurrent_hyperprior), alternating in one
-process.  GPU only.   python tools/step_ab.py [--reps 4] [--steps 10]"""
+"""A/B of a BASELINE config's training step (C2 default) with and without the hyperprior side
+stream (Compressor2018.concurrent_hyperprior), alternating in one process.  GPU only.
+    python tools/step_ab.py [--config C3] [--reps 4] [--steps 10]"""
 import argparse
 import os
 import sys
@@ -18,10 +18,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--config", default="C2")
     a = ap.parse_args()
+    conf = bench.CONFIGS[a.config]
     torch.manual_seed(0)
-    m = modelling.build_model(bench._cfg(conf=bench.CONFIGS["C2"])).cuda().train()
-    x = torch.rand(32, 3, 256, 256, device="cuda")
+    m = modelling.build_model(bench._cfg(conf=conf)).cuda().train()
+    x = torch.rand(conf["batch"], 3, conf["size"], conf["size"], device="cuda")
 
     def step():
         m.zero_grad(set_to_none=True)
