@@ -140,7 +140,8 @@ class Conv2dFn(Function):
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
         stride, padding, act, has_b, math = ctx.conf
-        pre = _take_colsum(gy) if (has_b and not act) else None  # bias gradient formed by gy's producer
+        # the bias gradient formed by gy's producer (taken only where this node owns the bias gradient)
+        pre = _take_colsum(gy) if (has_b and not act and ctx.needs_input_grad[2]) else None
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
@@ -177,7 +178,8 @@ class ConvTranspose2dFn(Function):
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
         stride, padding, act, has_b, math = ctx.conf
-        pre = _take_colsum(gy) if (has_b and not act) else None  # bias gradient formed by gy's producer
+        # the bias gradient formed by gy's producer (taken only where this node owns the bias gradient)
+        pre = _take_colsum(gy) if (has_b and not act and ctx.needs_input_grad[2]) else None
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
@@ -331,16 +333,20 @@ class _ConvWGradFn(Function):
         cur = torch.cuda.current_stream(x.device)
         x.record_stream(cur)   # x and the incoming gradient were allocated on the producing stream
         gz.record_stream(cur)
+        pre = _take_colsum(gz) if (ctx.has_b and not act) else None  # bias gradient formed by gz's producer
+        if pre is not None:
+            pre.record_stream(cur)
         gy = relu_bwd(ctx.holder["y"], gz) if act else gz
         gy = _cl(gy)
         ops, k = _lib.ops(), w.shape[2]
+        fb = ctx.has_b and pre is None
         if transposed:
-            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, ctx.has_b, math)
+            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, fb, math)
             _log_plan("conv_transpose2d_wgrad", x, gy, k, stride, padding, math)
         else:
-            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, ctx.has_b, math)
+            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, fb, math)
             _log_plan("conv2d_wgrad", x, gy, k, stride, padding, math)
-        return None, dw, (db if ctx.has_b else None), None, None, None
+        return None, dw, ((db if pre is None else pre) if ctx.has_b else None), None, None, None
 
 
 class _JoinFn(Function):
