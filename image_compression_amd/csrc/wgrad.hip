@@ -724,7 +724,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #define WG_X3_DUAL 1
 #endif
 #ifndef WG_X3G
-#define WG_X3G 0  // 1: 5x5 stride-2 192x192 weight gradients on the tap-group kernel (wg_x3g_kernel)
+#define WG_X3G 1  // 5x5 stride-2 192x192 weight gradients on the tap-group kernel (wg_x3g_kernel); 0: wg_x3d_kernel
 #endif
 #ifndef WG_X3_DUAL16
 #define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
