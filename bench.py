@@ -61,7 +61,8 @@ MATH_NOTE = {
                   "entropy models and the 3-channel edges on the fp32 MFMA / VALU",
     "fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain)",
     "bf16": "bf16 operands, fp32 accumulation (g_a/g_s conv fwd/dgrad/wgrad, GDN forward and backward "
-            "contractions); hyperprior and wgrad of maps < 16 wide in fp32_split; entropy models and edges fp32",
+            "contractions); hyperprior, the 3-channel image edges and wgrad of maps < 16 wide in fp32_split; "
+            "entropy models fp32",
 }
 BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
 # configs whose dominant kernel (g_a layer 2 fwd at 32 x 128^2) bench times live: C2 (fp32_split) and

@@ -225,7 +225,8 @@ KERNELS = {1: "ig_fp32", 2: "ig_fp32_gather", 3: "ig_bf16", 4: "ig_split", 5: "i
            7: "im2col_gemm", 8: "tconv_few", 9: "tconv_few_rows", 10: "gemm_col2im", 11: "wg_fp32",
            12: "wg_fp32_gather", 13: "wg_ldsdma", 14: "wg_split", 15: "edge_wgrad", 16: "gdn_fused",
            17: "gdn_fused_split", 18: "gdn_gemm", 20: "wg_bf16",
-           21: "gdn_fused_bf16", 22: "ig_split_dma"}
+           21: "gdn_fused_bf16", 22: "ig_split_dma", 23: "edge_conv_bf16", 24: "tconv_few_rows_bf16",
+           25: "edge_wgrad_bf16"}
 
 
 def plan(op, a, b=None, k=1, stride=1, pad=0, math=0):

@@ -10,6 +10,9 @@
 #include "../../include/imgcomp.h"
 #include "gemm.h"
 
+#ifndef EDGE_BF16
+#define EDGE_BF16 0  // 1: C3 (IC_MATH_BF16) runs the 3-channel image edges on bf16 operands too; 0: split arithmetic
+#endif
 #ifndef TAP_PARITY_ORDER
 #define TAP_PARITY_ORDER 1  // stride-2 direct convs walk even kernel rows first, then odd (conv_impl); 0: row order
 #endif
@@ -48,10 +51,12 @@ int direct_im2col(const ic_act* x, const float* W, const float* bias, int k, int
     // patch-gather kernel (edge.hip): no im2col columns in HBM
     const int Npad = ig_npad(y->c);
     const size_t wpb = (size_t)Npad * Kp * 4;
-    const int split = (math & IC_MATH_SPLIT) ? 1 : 0;
+    // 2: bf16 operands (C3), 1: split arithmetic, 0: fp32 MFMA
+    const int split = (EDGE_BF16 && (math & IC_MATH_BF16)) ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0;
     if (need) {
-      // variant 1: split arithmetic (edge_conv_x3_kernel)
-      plan_report(IC_KERNEL_EDGE_CONV, 64, y->c, 1, 0, 0, -1, edge_conv_split(split, T * x->c, y->c) ? 1 : 0);
+      // edge_conv_x3_kernel (variant 1) in split arithmetic or with bf16 operands
+      const bool x3 = edge_conv_split(split, T * x->c, y->c);
+      plan_report(x3 && split == 2 ? IC_KERNEL_EDGE_CONV_BF16 : IC_KERNEL_EDGE_CONV, 64, y->c, 1, 0, 0, -1, x3 ? 1 : 0);
       *need = ic_align(wpb, 256);
       return IC_OK;
     }
@@ -224,11 +229,12 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if ((epi == EPI_NONE || epi == EPI_RELU) &&
       tconv_few_ok(x->c, y->c, k, stride, pad, x->sc, x->sw, x->sh, x->sn, x->h, x->w)) {
     // output-row-stationary kernel (edge.hip): no column buffer in HBM
-    const int split = (math & IC_MATH_SPLIT) ? 1 : 0;
+    const int split = (EDGE_BF16 && (math & IC_MATH_BF16)) ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0;
     if (need) {
       const int kind = tconv_few_kind(x->h, x->w, k, pad, y->h);
-      // variant 1: the input-row kernel in split arithmetic
-      plan_report(kind, 0, y->c, 1, 0, 0, -1, (kind == IC_KERNEL_TCONV_FEW_ROWS && split && x->c % 32 == 0) ? 1 : 0);
+      // variant 1: the input-row kernel in split arithmetic or with bf16 operands
+      const bool x3 = kind == IC_KERNEL_TCONV_FEW_ROWS && split && x->c % 32 == 0;
+      plan_report(x3 && split == 2 ? IC_KERNEL_TCONV_FEW_ROWS_BF16 : kind, 0, y->c, 1, 0, 0, -1, x3 ? 1 : 0);
       *need = 0;
       return IC_OK;
     }
@@ -369,18 +375,21 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   // few X channels, wide NHWC G: patch-gather wgrad (edge.hip); the bias
   // gradient comes from its all-ones column when the bias belongs to G
   if (X->c <= FEW_CH && edge_wgrad_ok(X->c, k, stride, X->sw, G->data, G->c, G->sc, G->sw, G->sh, G->sn, G->h, G->w)) {
-    const bool db_from_g = db && bias_src->data == G->data;
+    const int split = (EDGE_BF16 && (math & IC_MATH_BF16)) ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0;
+    // the bias gradient from G's all-ones column, except with bf16 operands (it would sum rounded G)
+    const bool db_from_g = db && bias_src->data == G->data && split != 2;
     const int Kc = k * k * X->c + (db_from_g ? 1 : 0);
     const size_t slab = edge_wgrad_ws(G->c, Kc, edge_units(G->n, G->h, G->w));
     const size_t cs = (db && !db_from_g) ? colsum_ws((long long)bias_src->n * bias_src->h * bias_src->w, bias_src->c) : 0;
     if (need) {
-      plan_report(IC_KERNEL_EDGE_WGRAD, G->c, Kc, 1, 0, 0, -1, (math & IC_MATH_SPLIT) ? 1 : 0);  // 1: split
+      plan_report(split == 2 ? IC_KERNEL_EDGE_WGRAD_BF16 : IC_KERNEL_EDGE_WGRAD, G->c, Kc, 1, 0, 0, -1,
+                  split ? 1 : 0);  // 1: split arithmetic or bf16 operands
       *need = ic_align(slab, 256) + ic_align(cs, 256);
       return IC_OK;
     }
     if (wsb < ic_align(slab, 256) + ic_align(cs, 256)) return IC_ERR_WORKSPACE;
     int rc = edge_wgrad_run(G->data, G->c, X->data, X->sn, X->sc, X->sh, X->sw, X->n, X->c, X->h, X->w, G->h, G->w,
-                            k, stride, pad, dw, db_from_g ? db : nullptr, ws, s, (math & IC_MATH_SPLIT) ? 1 : 0);
+                            k, stride, pad, dw, db_from_g ? db : nullptr, ws, s, split);
     if (rc) return rc;
     if (db && !db_from_g)
       rc = colsum(bias_src->data, bias_src->sn, bias_src->sc, bias_src->sh, bias_src->sw, bias_src->n, bias_src->c,

@@ -250,14 +250,17 @@ __global__ void __launch_bounds__(256, EDGE_CONV_PER_CU)
 constexpr int EC3_S = 3;
 constexpr int EC3_KP = 32 * EC3_S;       // k columns of the B planes (96)
 constexpr int EC3_PL = SEG * EC3_KP;     // bf16 per plane
-template <int COUT>
+// NP = 1 (IC_MATH_BF16, config C3): bf16 operands (weights and patch values rounded to nearest
+// even), one plane, one product per tile and k-step, fp32 accumulation.
+template <int COUT, int NP = 3>
 __global__ void __launch_bounds__(512, 1)
     edge_conv_x3_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
                         int relu, float* __restrict__ y, long long ys_n, long long ys_h, long long ys_w) {
   typedef __bf16 eb4 __attribute__((ext_vector_type(4)));
   typedef __bf16 eb8 __attribute__((ext_vector_type(8)));
+  static_assert(NP == 3 || NP == 1, "split (3 planes) or bf16 (1 plane)");
   constexpr int NTW = COUT / 64;
-  __shared__ __attribute__((aligned(16))) __bf16 bpl[2 * 3 * EC3_PL];  // two units' B planes
+  __shared__ __attribute__((aligned(16))) __bf16 bpl[2 * NP * EC3_PL];  // two units' B planes
   __shared__ __attribute__((aligned(16))) float lds[2 * (PMAX + 2 * SEG * 2)];  // two patches
   __shared__ __attribute__((aligned(16))) float bl[COUT];  // bias (read per unit: frees 4 NTW VGPRs)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -270,7 +273,7 @@ __global__ void __launch_bounds__(512, 1)
   const int bufsz = PMAX + 2 * SEG * 2;
 
   // split weights as A fragments: aw[part][sx][j] = plane part of wp[n = nbase + 16 j + li][32 sx + 8 lq .. + 7]
-  eb8 aw[3][EC3_S][NTW];
+  eb8 aw[NP][EC3_S][NTW];
 #pragma unroll
   for (int sx = 0; sx < EC3_S; ++sx)
 #pragma unroll
@@ -279,11 +282,15 @@ __global__ void __launch_bounds__(512, 1)
       for (int e = 0; e < 8; ++e) {
         const int kq = 32 * sx + 8 * lq + e;
         const float v = (sx < S && kq < Kp) ? wp[(size_t)(nbase + 16 * j + li) * Kp + kq] : 0.f;
-        __bf16 hh, mm, ll;
-        split3_bf16(v, hh, mm, ll);
-        aw[0][sx][j][e] = hh;
-        aw[1][sx][j][e] = mm;
-        aw[2][sx][j][e] = ll;
+        if constexpr (NP == 1) {
+          aw[0][sx][j][e] = (__bf16)v;  // round to nearest even
+        } else {
+          __bf16 hh, mm, ll;
+          split3_bf16(v, hh, mm, ll);
+          aw[0][sx][j][e] = hh;
+          aw[NP - 2][sx][j][e] = mm;
+          aw[NP - 1][sx][j][e] = ll;
+        }
       }
   // plane build assignment: groups gi = tid + 512 q (q < 3) = (pixel gi / 24, k quad gi % 24)
   int bkoff[3][4], bdst[3];  // patch offsets of the group's 4 k at its pixel; plane offset
@@ -305,11 +312,16 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const floatx4v x = {patch[bkoff[q][0]], patch[bkoff[q][1]], patch[bkoff[q][2]], patch[bkoff[q][3]]};
-      eb4 h, m, l;
-      split3_bf16x4(x, h, m, l);
-      *(eb4*)(planes + bdst[q]) = h;
-      *(eb4*)(planes + EC3_PL + bdst[q]) = m;
-      *(eb4*)(planes + 2 * EC3_PL + bdst[q]) = l;
+      if constexpr (NP == 1) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        *(eb4*)(planes + bdst[q]) = __builtin_bit_cast(eb4, u32x2{ic_cvt_pk_bf16(x[0], x[1]), ic_cvt_pk_bf16(x[2], x[3])});
+      } else {
+        eb4 h, m, l;
+        split3_bf16x4(x, h, m, l);
+        *(eb4*)(planes + bdst[q]) = h;
+        *(eb4*)(planes + EC3_PL + bdst[q]) = m;
+        *(eb4*)(planes + 2 * EC3_PL + bdst[q]) = l;
+      }
     }
   };
 
@@ -342,8 +354,8 @@ __global__ void __launch_bounds__(512, 1)
     __syncthreads();
     const long long u2 = u + 2 * gs;
     edge_patch_load(g, pm, min(u2, ulast), pr);
-    build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * 3 * EC3_PL);
-    const __bf16* planes = bpl + (it & 1) * 3 * EC3_PL;
+    build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
+    const __bf16* planes = bpl + (it & 1) * NP * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -356,16 +368,22 @@ __global__ void __launch_bounds__(512, 1)
         for (int t = 0; t < 2; ++t) {
           const int p = 16 * (mt0 + t) + li;
           const int off = p * EC3_KP + 8 * ((4 * sx + lq) ^ (((p >> 3) & 1) << 1));
-          eb8 bf[3];
+          eb8 bf[NP];
 #pragma unroll
-          for (int q = 0; q < 3; ++q) bf[q] = *(const eb8*)(planes + q * EC3_PL + off);
-          // the six products, smallest first (a dependent MFMA issues back to back)
-          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+          for (int q = 0; q < NP; ++q) bf[q] = *(const eb8*)(planes + q * EC3_PL + off);
+          if constexpr (NP == 1) {
 #pragma unroll
-          for (int j = 0; j < NTW; ++j)
+            for (int j = 0; j < NTW; ++j)
+              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][sx][j], bf[0], acc[t][j], 0, 0, 0);
+          } else {
+            // the six products, smallest first (a dependent MFMA issues back to back)
+            constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-            for (int pr6 = 0; pr6 < 6; ++pr6)
-              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[PA[pr6]][sx][j], bf[PB[pr6]], acc[t][j], 0, 0, 0);
+            for (int j = 0; j < NTW; ++j)
+#pragma unroll
+              for (int pr6 = 0; pr6 < 6; ++pr6)
+                acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[PA[pr6]][sx][j], bf[PB[pr6]], acc[t][j], 0, 0, 0);
+          }
         }
       }
     }
@@ -409,7 +427,9 @@ __global__ void __launch_bounds__(512, 1)
 // the same LDS reads of G and of the patch as the fp32 loop (k-slot e of lane
 // group lq takes pixel 32 ks + 4e + lq, so one read instruction spans four
 // consecutive, differently swizzled G rows), split in registers.
-template <int CG, int KTMAX, bool X3>
+// NP = 1 with X3 (IC_MATH_BF16, config C3): G and the patch values rounded to nearest even, one
+// product per tile and 32-pixel step, fp32 accumulation.
+template <int CG, int KTMAX, bool X3, int NP = 3>
 __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     edge_wgrad_kernel(const EdgeGeom g, const float* __restrict__ G, int Kc, int ones, float* __restrict__ slab) {
   typedef __bf16 eb4 __attribute__((ext_vector_type(4)));
@@ -483,6 +503,12 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
     const float* patch = pbase + buf * PB;
     if constexpr (X3) {
       auto split8 = [](const float (&v)[8], eb8& h, eb8& m, eb8& l) {
+        if constexpr (NP == 1) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          h = __builtin_bit_cast(eb8, u32x4{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3]),
+                                            ic_cvt_pk_bf16(v[4], v[5]), ic_cvt_pk_bf16(v[6], v[7])});
+          return;
+        }
         eb4 h0, m0, l0, h1, m1, l1;
         split3_bf16x4(floatx4v{v[0], v[1], v[2], v[3]}, h0, m0, l0);
         split3_bf16x4(floatx4v{v[4], v[5], v[6], v[7]}, h1, m1, l1);
@@ -515,6 +541,10 @@ __global__ void __launch_bounds__(256, KTMAX <= 5 ? 2 : 1)
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
               floatx4v& c = acc[i][kt];
+              if constexpr (NP == 1) {
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+                continue;
+              }
               c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
               c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
               c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
@@ -766,7 +796,9 @@ constexpr int TF2_WSEG = 120;
 // [ky][s][part][lq][col][8] (8 consecutive channels 32s + 8lq + e of column
 // col per lane: one b128 read per part), and each lane splits its pixel's
 // 8-channel A fragment per 32-channel step from the same row registers.
-template <int NWV, bool X3>
+// NP = 1 with X3 (IC_MATH_BF16, config C3): bf16 operands (weights and the pixel's channels rounded
+// to nearest even), one product per tap row and 32-channel step, fp32 accumulation.
+template <int NWV, bool X3, int NP = 3>
 __global__ void __launch_bounds__(64 * NWV, 1)
     tconv_few2_kernel(const float* __restrict__ x, int N, int Hin, int Win, int Cin, const float* __restrict__ W,
                       int Cout, int k, int pad, const float* __restrict__ bias, int relu, float* __restrict__ y,
@@ -796,12 +828,16 @@ __global__ void __launch_bounds__(64 * NWV, 1)
         const int kx = col / Cout, o = col - (col / Cout) * Cout;
         val = W[(((size_t)c * Cout + o) * k + ky) * k + kx];
       }
-      __bf16 hh, mm, ll;
-      split3_bf16(val, hh, mm, ll);
       const int o0 = (ky * S + sx) * 3 * PART + (q * 16 + col) * 8 + e;
-      wb[o0] = hh;
-      wb[o0 + PART] = mm;
-      wb[o0 + 2 * PART] = ll;
+      if constexpr (NP == 1) {
+        wb[o0] = (__bf16)val;  // round to nearest even
+      } else {
+        __bf16 hh, mm, ll;
+        split3_bf16(val, hh, mm, ll);
+        wb[o0] = hh;
+        wb[o0 + PART] = mm;
+        wb[o0 + 2 * PART] = ll;
+      }
     }
   } else {
     for (int i = tid; i < k * U * 4 * 16 * 4; i += NT) {
@@ -881,7 +917,19 @@ __global__ void __launch_bounds__(64 * NWV, 1)
     if (X3 && r >= 0 && r < Hin) {
 #pragma unroll
       for (int sx = 0; sx < 6; ++sx) {
-        if (sx < S) {
+        if (sx < S && NP == 1) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const floatx4v v0 = a[2 * sx], v1 = a[2 * sx + 1];
+          const tb8 ab = __builtin_bit_cast(tb8, u32x4{ic_cvt_pk_bf16(v0[0], v0[1]), ic_cvt_pk_bf16(v0[2], v0[3]),
+                                                       ic_cvt_pk_bf16(v1[0], v1[1]), ic_cvt_pk_bf16(v1[2], v1[3])});
+#pragma unroll
+          for (int ky = 0; ky < 5; ++ky) {
+            if (ky < k) {
+              const tb8 b0 = *(const tb8*)(wb + (ky * S + sx) * 3 * PART + (lq * 16 + li) * 8);
+              acc[ky] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, b0, acc[ky], 0, 0, 0);
+            }
+          }
+        } else if (sx < S) {
           tb4 h0, m0, l0, h1, m1, l1;
           split3_bf16x4(a[2 * sx], h0, m0, l0);
           split3_bf16x4(a[2 * sx + 1], h1, m1, l1);
@@ -964,15 +1012,19 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
   if (edge_conv_split(split, g.TC, Cout)) {
     const int grid1 = edge_grid(g.units, 1);
     if (grid1 < 1) return IC_OK;
-    if (Cout == 192)
-      hipLaunchKernelGGL(edge_conv_x3_kernel<192>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
-                         ys_h, ys_w);
-    else if (Cout == 128)
-      hipLaunchKernelGGL(edge_conv_x3_kernel<128>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
-                         ys_h, ys_w);
-    else
-      hipLaunchKernelGGL(edge_conv_x3_kernel<64>, dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, ys_n,
-                         ys_h, ys_w);
+#define EDGE_CONV_X3(CO_)                                                                                      \
+  do {                                                                                                         \
+    if (split == 2)                                                                                            \
+      hipLaunchKernelGGL((edge_conv_x3_kernel<CO_, 1>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, \
+                         ys_n, ys_h, ys_w);                                                                    \
+    else                                                                                                       \
+      hipLaunchKernelGGL((edge_conv_x3_kernel<CO_>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y,    \
+                         ys_n, ys_h, ys_w);                                                                    \
+  } while (0)
+    if (Cout == 192) EDGE_CONV_X3(192);
+    else if (Cout == 128) EDGE_CONV_X3(128);
+    else EDGE_CONV_X3(64);
+#undef EDGE_CONV_X3
     IC_CHECK_LAUNCH();
     return IC_OK;
   }
@@ -1037,8 +1089,11 @@ int edge_wgrad_run(const float* G, int CG, const float* x, long long sn, long lo
   const bool x3 = EW_SPLIT && split;
 #define EDGE_WG(CG_, KT_)                                                                                       \
   do {                                                                                                          \
-    if (x3) hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, true>), dim3(grid), dim3(256), 0, s, g, G, Kc,     \
-                               db ? 1 : 0, slab);                                                               \
+    if (x3 && split == 2)                                                                                       \
+      hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, true, 1>), dim3(grid), dim3(256), 0, s, g, G, Kc,         \
+                         db ? 1 : 0, slab);                                                                     \
+    else if (x3) hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, true>), dim3(grid), dim3(256), 0, s, g, G, Kc,\
+                                    db ? 1 : 0, slab);                                                          \
     else hipLaunchKernelGGL((edge_wgrad_kernel<CG_, KT_, false>), dim3(grid), dim3(256), 0, s, g, G, Kc,       \
                             db ? 1 : 0, slab);                                                                  \
   } while (0)
@@ -1093,7 +1148,10 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
     if (run > Hin) run = Hin;
     const long long blocks = (long long)N * ((Hin + run - 1) / run) * nseg;
     if (blocks >= (1LL << 31)) return IC_ERR_ARG;
-    if (TF2_SPLIT && split && Cin % 32 == 0)
+    if (TF2_SPLIT && split == 2 && Cin % 32 == 0)
+      hipLaunchKernelGGL((tconv_few2_kernel<8, true, 1>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin,
+                         W, Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run, wseg);
+    else if (TF2_SPLIT && split && Cin % 32 == 0)
       hipLaunchKernelGGL((tconv_few2_kernel<8, true>), dim3((unsigned)blocks), dim3(512), 0, s, x, N, Hin, Win, Cin, W,
                          Cout, k, pad, bias, relu, y, ysn, ysc, ysh, ysw, Hout, Wout, (int)run, wseg);
     else

@@ -22,13 +22,14 @@ def set_compute_dtype(model, dtype):
     (functional.MATH) — for the forward, input gradient and weight gradient of
     every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16 operands with fp32
     accumulation (reduced precision, BASELINE config C3) for the forward, input
-    gradient and weight gradient of the main transforms (g_a, g_s) — 97 % of the
-    model's FLOPs; where a bf16 kernel does not apply (weight gradients of maps
+    gradient and weight gradient of the main transforms (g_a, g_s; their 3-channel
+    image edges too when the library is built with EDGE_BF16) — 97 % of the model's
+    FLOPs; where a bf16 kernel does not apply (weight gradients of maps
     narrower than 16) they fall back to "fp32_split", and the hyperprior
     transforms (1.3 % of the FLOPs, but they shape the rate term's gradients)
-    run in "fp32_split" arithmetic there.  GDN,
-    the entropy models and the 3-channel image edges compute in fp32 in every
-    mode, except that "fp32_split" runs GDN (C = 192) in split arithmetic too:
+    run in "fp32_split" arithmetic there.  GDN and
+    the entropy models compute in fp32 in every mode, except that "fp32_split"
+    runs GDN (C = 192) in split arithmetic too:
     the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at 128^2) and the fused
     backward's dgamma GEMM (GDN.math = 2: 4 % faster; A/B in one process,
     tools/gdn_ab.py), and "bf16" runs both of the backward's contractions and the

@@ -126,19 +126,31 @@ def check_relu_ties(masks, ctl, tau=1e-4):
     return flips
 
 
-BF16_KERNELS = ("ig_bf16", "ig_split_bf16", "wg_bf16", "gdn_fused_bf16")
+BF16_KERNELS = ("ig_bf16", "ig_split_bf16", "wg_bf16", "gdn_fused_bf16", "edge_conv_bf16", "tconv_few_rows_bf16",
+                "edge_wgrad_bf16")
 
 
-def c3_bf16_flags(n, size, latent):
+def edges_bf16():
+    """Whether this build runs C3's 3-channel image edges on bf16 operands (csrc/conv_api.hip
+    EDGE_BF16), from the library's own plan query (no launch)."""
+    from image_compression_amd import _lib
+    img = _lib.ICAct(256, 2, 3, 64, 64, 3 * 64 * 64, 64 * 64, 64, 1)
+    x = _lib.ICAct(256, 2, 192, 32, 32, 192 * 32 * 32, 1, 32 * 192, 192)
+    return _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 3)["kernel"] == "edge_conv_bf16"
+
+
+def c3_bf16_flags(n, size, latent, edges=None):
     """Which GEMMs of the main transforms take bf16 operands in the "bf16" compute dtype
     (BASELINE config C3), per weight name: (forward, input gradient, weight gradient) — the
     rule of csrc/conv_api.hip and csrc/wgrad.hip wg_plan, restated: conv / transposed-conv
     forward and input gradient on the implicit GEMM when the reduction channels are a multiple
-    of 64 and neither side is a 3-channel image edge; weight gradients when both channel counts
+    of 64; weight gradients when both channel counts
     are >= 128 and the output-gradient grid (transposed: the input grid) is >= 16 wide with
-    row-aligned 32-pixel steps; the GDN backward's two contractions (csrc/gdn_fused.hip BF).  Returns (flags for oracle.ref_cpu's bf16 emulation, the number
+    row-aligned 32-pixel steps; the 3-channel image edges (csrc/edge.hip, NP = 1) in every GEMM they
+    run when the build has them on (edges_bf16); the GDN forward's Gamma x^2 and the backward's two contractions (csrc/gdn_fused.hip).  Returns (flags for oracle.ref_cpu's bf16 emulation, the number
     of bf16 launches one training step makes)."""
     flags, launches = {}, 0
+    e = edges_bf16() if edges is None else edges
 
     def wg_ok(cg, cx, w_, p_):
         return cg >= 128 and cx >= 128 and w_ % 16 == 0 and (w_ % 32 == 0 or p_ % 32 == 0)
@@ -146,13 +158,18 @@ def c3_bf16_flags(n, size, latent):
     ch = [3, 192, 192, 192, latent]
     for i in range(4):  # analysis: conv ch[i] -> ch[i+1], output size / 2^(i+1)
         cin, cout, wo = ch[i], ch[i + 1], size >> (i + 1)
-        f = (cin % 64 == 0, i > 0 and cout % 64 == 0, cin > 4 and wg_ok(cout, cin, wo, n * wo * wo))
+        # the 3-channel image edge (i = 0) on the edge kernels: forward and weight gradient (the
+        # image needs no gradient)
+        f = (cin % 64 == 0 or (e and cin <= 4), i > 0 and cout % 64 == 0,
+             (e and cin <= 4) or (cin > 4 and wg_ok(cout, cin, wo, n * wo * wo)))
         flags[f"analysis_transform.layers.{2 * i}.weight"] = f
         launches += sum(f)
     ch = [latent, 192, 192, 192, 3]
     for i in range(4):  # synthesis: tconv ch[i] -> ch[i+1], input size / 2^(4-i)
         cin, cout, wi = ch[i], ch[i + 1], size >> (4 - i)
-        f = (cin % 64 == 0 and cout > 4, cout % 64 == 0, cout > 4 and wg_ok(cin, cout, wi, n * wi * wi))
+        # the image edge (cout 3): forward, input and weight gradient on the edge kernels
+        f = (cin % 64 == 0 and (e or cout > 4), cout % 64 == 0 or (e and cout <= 4),
+             (e and cout <= 4) or (cout > 4 and wg_ok(cin, cout, wi, n * wi * wi)))
         flags[f"synthesis_transform.layers.{2 * i}.weight"] = f
         launches += sum(f)
     # every GDN (C = 192, NHWC-dense: the fused kernels) has a bf16 forward and backward

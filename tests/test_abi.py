@@ -173,6 +173,13 @@ def test_plan_query_c2_instances():
     img = _act(32, 3, 256, 256, cl=False)
     assert _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 2)["kernel"] == "edge_conv"
     assert _lib.plan("conv_transpose2d_fwd", x, img, 5, 2, 2, 2)["kernel"] == "tconv_few_rows"
+    # C3 (split | bf16): the image edges on bf16 operands when the build has them on (EDGE_BF16)
+    bf = _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 3)["kernel"] == "edge_conv_bf16"
+    sfx = "_bf16" if bf else ""
+    assert _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 3)["kernel"] == "edge_conv" + sfx
+    assert _lib.plan("conv_transpose2d_fwd", x, img, 5, 2, 2, 3)["kernel"] == "tconv_few_rows" + sfx
+    assert _lib.plan("conv2d_wgrad", img, x, 5, 2, 2, 3)["kernel"] == "edge_wgrad" + sfx
+    assert _lib.plan("conv2d_wgrad", img, x, 5, 2, 2, 2)["kernel"] == "edge_wgrad"
     assert _lib.plan("gdn_fwd", x, math=2)["kernel"] == "gdn_fused_split"
     assert _lib.plan("gdn_fwd", x, math=3)["kernel"] == "gdn_fused_bf16"   # C3: split | bf16
     assert _lib.plan("gdn_bwd", x, math=3)["kernel"] == "gdn_fused_bf16"

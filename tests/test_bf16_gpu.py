@@ -99,6 +99,61 @@ def test_tconv_bf16_fwd_dgrad():
     assert 1e-5 < rel_err(xd.grad.cpu(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("transposed", [False, True])
+def test_image_edges_bf16(transposed):
+    """C3's 3-channel image edges on bf16 operands (edge_conv_x3_kernel / tconv_few2_kernel /
+    edge_wgrad_kernel with one product): g_a.0 (conv 3 -> 192) forward and weight gradient, g_s.6
+    (transposed conv 192 -> 3) forward, input gradient and weight gradient, against the fp64 oracle
+    of the same bf16-rounded operands (oracle.ref_cpu._ConvRounded, the C3 emulation: within
+    1e-5) and against exact fp64 (within the 1e-2 bf16 bar, above 1e-5: the operands were rounded);
+    the plans name the bf16 edge kernels."""
+    from conftest import edges_bf16
+    from image_compression_amd import _lib
+    from image_compression_amd import functional as IF
+    from oracle import ref_cpu
+    if not edges_bf16():
+        pytest.skip("this build runs the image edges in split arithmetic in C3 (EDGE_BF16 = 0)")
+    m = IF.MATH["bf16"] | IF.MATH["fp32_split"]   # what set_compute_dtype gives the main transforms in C3
+    if transposed:
+        x = _r(2, 192, 16, 24, seed=21)
+        w = _r(192, 3, 5, 5, seed=22, scale=0.05)
+        xd = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        wd = w.to(DEV).requires_grad_(True)
+        y = IF.conv_transpose2d(xd, wd, None, 2, 2, 1, math=m)
+        kinds = [_lib.plan("conv_transpose2d_fwd", xd, y, 5, 2, 2, m)["kernel"],
+                 _lib.plan("conv_transpose2d_wgrad", xd, y, 5, 2, 2, m)["kernel"]]
+        assert kinds == ["tconv_few_rows_bf16", "edge_wgrad_bf16"], kinds
+    else:
+        x = _r(2, 3, 40, 72, seed=21)
+        w = _r(192, 3, 5, 5, seed=22, scale=0.2)
+        xd = x.to(DEV).requires_grad_(False)
+        wd = w.to(DEV).requires_grad_(True)
+        y = IF.conv2d(xd, wd, None, 2, 2, math=m)
+        kinds = [_lib.plan("conv2d_fwd", xd, y, 5, 2, 2, m)["kernel"], _lib.plan("conv2d_wgrad", xd, y, 5, 2, 2, m)["kernel"]]
+        assert kinds == ["edge_conv_bf16", "edge_wgrad_bf16"], kinds
+    gy = _r(*y.shape, seed=23)
+    y.backward(gy.to(DEV))
+    outs = {"y": y.detach().cpu(), "dw": wd.grad.cpu()}
+    if transposed:
+        outs["dx"] = xd.grad.cpu()
+    for flags in ((True, True, True), None):
+        xr = x.double().requires_grad_(transposed)
+        wr = w.double().requires_grad_(True)
+        yr = ref_cpu._conv(xr, wr, None, 2, 2, "w", {"w": flags} if flags else None, transposed=transposed,
+                           opad=1 if transposed else 0)
+        yr.backward(gy.double())
+        refs = {"y": yr.detach(), "dw": wr.grad}
+        if transposed:
+            refs["dx"] = xr.grad
+        for k, ref in refs.items():
+            e = rel_err(outs[k], ref)
+            print(f"edge bf16 transposed={transposed} {k}: vs {'emulation' if flags else 'exact fp64'} {e:.2e}")
+            if flags:
+                assert e < 1e-5, (k, e)
+            else:
+                assert 1e-5 < e < 1e-2, (k, e)
+
+
 def test_model_c3_bf16_vs_oracle():
     from image_compression_amd import functional as IF, get_cfg_defaults, injected_noise, modelling
     cfg = get_cfg_defaults()

@@ -6,7 +6,7 @@ TAG=${1:-run}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
+timeout -k 10 600 python -m pytest tests -m gpu -q -rf -s -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
 echo "TESTS EXIT $?" | tee -a gpurun_out/tests_$TAG.log
 rc=$(tail -1 gpurun_out/tests_$TAG.log | awk '{print $3}')
 case $rc in 0|1) ;; *) echo "abort after tests rc=$rc"; exit $rc;; esac
