@@ -11,7 +11,7 @@
 #include "gemm.h"
 
 #ifndef EDGE_BF16
-#define EDGE_BF16 0  // 1: C3 (IC_MATH_BF16) runs the 3-channel image edges on bf16 operands too; 0: split arithmetic
+#define EDGE_BF16 1  // C3 (IC_MATH_BF16): the 3-channel image edges on bf16 operands too; 0: split arithmetic
 #endif
 #ifndef TAP_PARITY_ORDER
 #define TAP_PARITY_ORDER 1  // stride-2 direct convs walk even kernel rows first, then odd (conv_impl); 0: row order
