@@ -17,5 +17,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAIL; tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
 # the dominant kernel's launches the roofline times live (g_a.2 fwd: the first main-queue ig_kernel_x3d of each
 # step) from the same trace, to set beside bench's live figure
-python3 $R/tools/trace_timeline.py $(find $R/gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1) --first ig_kernel_x3d | head -2
+python3 $R/tools/trace_timeline.py $(find $R/gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1) --first ig_kernel_x3d > $R/gpurun_out/first_$TAG.txt 2>&1
+head -2 $R/gpurun_out/first_$TAG.txt
 echo DONE
