@@ -23,9 +23,6 @@
 // 64-channel-chunk kernel keeps the 128-row tiles: 0.378 vs 0.412 ms on g_a.2)
 #define IG_BF16_S 1
 #endif
-#ifndef IG_BF16_BM256
-#define IG_BF16_BM256 0  // 1: bf16 operands on 256-row 8-wave tiles of ig_kernel_bf16 where they fill the chip
-#endif
 #ifndef IG_BF16_NARROW
 #define IG_BF16_NARROW 0  // 1: bf16 operands on the 32-channel-chunk kernel at 128-row tiles too
 #endif
@@ -330,15 +327,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM / WM) * (BN / WN) == 8 ? 1 : 2)
-    ig_kernel_bf16(const IgDesc d) {
+__global__ void __launch_bounds__(256, 2) ig_kernel_bf16(const IgDesc d) {
   constexpr int LDKB = 72;
   constexpr int WAVES_N = BN / WN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int NT = 64 * (BM / WM) * (BN / WN);
-  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
-  constexpr int AROWS = NT / 16, BROWS = NT / 8;  // rows staged per pass: 16 float4 / 8 x 16 B per row
-  constexpr int APASS = BM / AROWS, BPASS = BN / BROWS;
+  constexpr int APASS = BM / 16, BPASS = BN / 32;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
   __shared__ __attribute__((aligned(16))) __bf16 As[BM * LDKB];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * LDKB];
 
@@ -366,7 +360,7 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM / WM) * (BN / 
   int a_iy[APASS], a_ix[APASS];
 #pragma unroll
   for (int p = 0; p < APASS; ++p) {
-    const uint32_t m = m0 + arow + AROWS * p;
+    const uint32_t m = m0 + arow + 16 * p;
     const bool ok = m < M;
     const uint32_t mm = ok ? m : 0u;
     const uint32_t img = fdiv(mm, P.fd_hw);
@@ -395,17 +389,17 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM / WM) * (BN / 
     }
     const __bf16* wb = wpb + ((size_t)t * d.Npad + n0 + brow) * d.Cin + cc * 64 + bc8 * 8;
 #pragma unroll
-    for (int p = 0; p < BPASS; ++p) rb[p] = *(const bf16x8*)(wb + (size_t)(BROWS * p) * d.Cin);
+    for (int p = 0; p < BPASS; ++p) rb[p] = *(const bf16x8*)(wb + (size_t)(32 * p) * d.Cin);
   };
   auto sstore = [&]() {
 #pragma unroll
     for (int p = 0; p < APASS; ++p) {
       bf16x4 v;
       v[0] = (__bf16)ra[p][0]; v[1] = (__bf16)ra[p][1]; v[2] = (__bf16)ra[p][2]; v[3] = (__bf16)ra[p][3];
-      *(bf16x4*)&As[(arow + AROWS * p) * LDKB + ac4 * 4] = v;
+      *(bf16x4*)&As[(arow + 16 * p) * LDKB + ac4 * 4] = v;
     }
 #pragma unroll
-    for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[(brow + BROWS * p) * LDKB + bc8 * 8] = rb[p];
+    for (int p = 0; p < BPASS; ++p) *(bf16x8*)&Bs[(brow + 32 * p) * LDKB + bc8 * 8] = rb[p];
   };
 
   const int lane = tid & 63, w = tid >> 6;
@@ -1045,11 +1039,6 @@ size_t ig_plan(IgDesc& d) {
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
   else { d.bm = 256; d.bn = 32; }
-  if (IG_BF16_BM256 && d.bf16 && d.bn == 192 && d.bm == 128 && !d.generic && d.Cin % 64 == 0) {
-    long long t256 = 0;
-    for (int p = 0; p < d.nphase; ++p) t256 += ic_cdiv((long long)d.N * d.ph[p].Hg * d.ph[p].Wg, 256);
-    if (t256 >= 256) d.bm = 256;
-  }
   if (d.bn % 64 != 0) d.x3 = 0;  // the split kernel stages B 64 rows per pass; native fp32 instead
   d.Npad = ig_npad(d.Cout);
   long long mtot = 0;
@@ -1118,14 +1107,6 @@ int ig_run(IgDesc& d, hipStream_t s) {
     for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
     if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
     hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
-    IC_CHECK_LAUNCH();
-    rc = IC_OK;
-  }
-  else if (d.bn == 192 && d.bm == 256 && d.bf16) {
-    int mt = 0;
-    for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
-    if (d.a_op == AOP_SQUARE || !ig_bf16_wide(d)) return IC_ERR_ARG;
-    hipLaunchKernelGGL((ig_kernel_bf16<256, 192, 64, 96>), dim3(mt, d.Npad / 192, d.nphase * d.ksplit), dim3(512), 0, s, d);
     IC_CHECK_LAUNCH();
     rc = IC_OK;
   }
