@@ -38,12 +38,15 @@ class _StreamEdge(torch.autograd.Function):
 
 
 def side_stream(device):
-    """One high-priority side stream per device for the hyperprior branch, and beside it a
-    normal-priority stream for the hyperprior convs' weight gradients (functional: convs run on the
-    side stream compute them there, off the chain of input gradients g_a's backward waits for)."""
+    """One side stream per device for the hyperprior branch, and beside it a stream for the
+    hyperprior convs' weight gradients (functional: convs run on the side stream compute them there,
+    off the chain of input gradients g_a's backward waits for).  Both at normal priority: a
+    high-priority side stream dispatched its blocks ahead of the main stream's critical kernels
+    whenever a CU freed up (C3 6.44 -> 6.35 ms per step at normal priority, C2 equal; r05s,
+    profiles/r05s_side_priority_ab.txt)."""
     k = device.index if device.index is not None else torch.cuda.current_device()
     if k not in _SIDE:
-        _SIDE[k] = torch.cuda.Stream(device=device, priority=-1)
+        _SIDE[k] = torch.cuda.Stream(device=device, priority=0)
         _WGRAD[k] = torch.cuda.Stream(device=device, priority=0)
         route_weight_gradients(_SIDE[k], _WGRAD[k])
     return _SIDE[k]
