@@ -56,14 +56,28 @@ CONFIGS = {
                gflop=73.70),
 }
 MATH_NOTE = {
-    "fp32_split": "fp32 via exact 3-term bf16 operand split, 6 products on v_mfma_f32_16x16x32_bf16, fp32 "
-                  "accumulation (fp32 fma-chain error): wide conv fwd/dgrad/wgrad, GDN (C=192) fwd and dgamma; "
-                  "entropy models and the 3-channel edges on the fp32 MFMA / VALU",
+    "fp32_split": "fp32 via exact 3-term bf16 operand split, 6 products on the bf16 MFMA, fp32 "
+                  "accumulation (fp32 fma-chain error): wide conv fwd/dgrad/wgrad, GDN (C=192) forward and both "
+                  "backward contractions, the 3-channel edges; entropy models on the fp32 MFMA / VALU",
     "fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain)",
     "bf16": "bf16 operands, fp32 accumulation (g_a/g_s conv fwd/dgrad/wgrad, GDN forward and backward "
-            "contractions); hyperprior, the 3-channel image edges and wgrad of maps < 16 wide in fp32_split; "
+            "contractions{edges}); hyperprior{edges_split} and wgrad of maps < 16 wide in fp32_split; "
             "entropy models fp32",
 }
+
+
+def _math_note(math):
+    """MATH_NOTE of `math`; for bf16, where the 3-channel image edges run is read from the built
+    library's plan (csrc/conv_api.hip EDGE_BF16; the query launches nothing)."""
+    note = MATH_NOTE[math]
+    if math == "bf16":
+        from image_compression_amd import _lib
+        img = _lib.ICAct(256, 2, 3, 64, 64, 3 * 64 * 64, 64 * 64, 64, 1)
+        x = _lib.ICAct(256, 2, 192, 32, 32, 192 * 32 * 32, 1, 32 * 192, 192)
+        on = _lib.plan("conv2d_fwd", img, x, 5, 2, 2, 3)["kernel"] == "edge_conv_bf16"
+        note = note.format(edges=", the 3-channel image edges" if on else "",
+                           edges_split="" if on else ", the 3-channel image edges")
+    return note
 BF16_PEAK_TFLOPS = 2500.0         # MI355X dense bf16 MFMA spec
 # configs whose dominant kernel (g_a layer 2 fwd at 32 x 128^2) bench times live: C2 (fp32_split) and
 # C3 (bf16 operands; same layer shape, the latent width does not touch it)
@@ -285,10 +299,10 @@ def main():
     ap.add_argument("--profile-step-only", action="store_true",
                     help="only warmup+timed steps (for rocprofv3 runs)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the step from a hipGraph (TrainStep; N > 1: one flat RCCL all-reduce "
-                         "after the replay) instead of eager launches (N > 1: DDP, 12 MB buckets "
-                         "overlapped with the backward).  Measured equal at N=1: the GPU, not the host, "
-                         "paces the launches.")
+                    help="one GPU only: replay the step from a hipGraph (TrainStep) instead of eager "
+                         "launches.  Slower than eager (about 20 us of runtime cost per graph node, "
+                         "DESIGN.md 10b); the multi-GPU path is eager DDP with 12 MB buckets overlapped "
+                         "with the backward, never a graph replay followed by an unbucketed all-reduce.")
     ap.add_argument("--math", default=None, choices=["fp32", "fp32_split", "bf16"],
                     help="override the config's cfg.MODEL.COMPUTE_DTYPE")
     args = ap.parse_args()
@@ -302,6 +316,8 @@ def main():
     from image_compression_amd import modelling
     rank, world, dev = D.setup()
     dist = world > 1
+    if args.graph and dist:
+        raise SystemExit("bench.py --graph is single-GPU only (see --help)")
     from image_compression_amd.step import TrainStep
     torch.manual_seed(0)
     model = modelling.build_model(_cfg(conf=conf)).to(dev).train()
@@ -318,10 +334,9 @@ def main():
             return losses
         mode = "eager, DDP 12 MB buckets" if dist else "eager"
     else:
-        # fwd + loss + bwd captured once into a hipGraph and replayed; for N > 1
-        # the flat gradient is all-reduced (RCCL) after each replay
+        # fwd + loss + bwd captured once into a hipGraph and replayed (one GPU)
         step = TrainStep(model, x, graph=True)
-        mode = "hipGraph" + (" + RCCL all-reduce of the flat gradient" if dist else "")
+        mode = "hipGraph"
 
     live = None
     if not args.graph and args.config in ROOFLINE_CONFIGS and not args.no_roofline:
@@ -374,7 +389,7 @@ def main():
             "config": {"workload": f"{args.config}: {conf['desc']}, "
                                    f"{args.size}x{args.size}, {args.batch} images/GPU, fwd+loss+bwd"
                                    + (" + grad all-reduce" if dist else "") + f" [{mode}]",
-                       "math": f"{conf['math']}: {MATH_NOTE[conf['math']]}",
+                       "math": f"{conf['math']}: {_math_note(conf['math'])}",
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(step_tflops, 2),

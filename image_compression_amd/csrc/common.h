@@ -68,8 +68,9 @@ __device__ __forceinline__ void split3_bf16(float a, __bf16& h, __bf16& m, __bf1
 #endif
 // split3_bf16 of four values with the bf16 conversions paired
 // (v_cvt_pk_bf16_f32 on two operands, round-to-nearest-even as the scalar
-// cast) and the residuals on v_pk_add_f32: 18 VALU per four values instead
-// of the 24 the compiler emits for four scalar splits.  Bitwise identical to
+// cast); the residuals are written as two-wide vector subtractions, which the
+// build lowers to scalar v_sub_f32 (every source is compiled without the
+// packed-fp32 instructions, csrc/Makefile NOPK).  Bitwise identical to
 // split3_bf16.  V4 is any 8-byte vector of four bf16.
 __device__ __forceinline__ uint32_t ic_cvt_pk_bf16(float lo, float hi) {
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));

@@ -165,8 +165,9 @@ __global__ void fact_fwd_k(const float* z, long long n, int C, const ic_fact_par
 
 __global__ void __launch_bounds__(256) fact_bwd_k(const float* qin, long long n, int C, const ic_fact_params P,
                            const float* dq, const float* dp, float* dz, const ic_fact_grads GR, int round_mode) {
-  // built without packed-fp32 VALU instructions (Makefile NOPK_SRCS): with them this kernel
-  // sometimes returned a wrong w1 / w2 gradient element while MFMA kernels shared its CUs
+  // built without packed-fp32 VALU instructions, like every source (Makefile NOPK): with them this
+  // kernel sometimes returned wrong w1 / w2 gradient sums in concurrent model steps (a mitigation,
+  // DESIGN.md section 10a)
   __shared__ float lds[16 * NG];
   const int c = blockIdx.x;
   ChanParams q;

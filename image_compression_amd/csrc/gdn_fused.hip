@@ -53,6 +53,9 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef GDN_BWD_DMA_B
 #define GDN_BWD_DMA_B 1  // fused backward: group B issues the next tile's DMA (0: group A, after its first MFMAs)
 #endif
+#ifndef GDN_BWD_X3W
+#define GDN_BWD_X3W 1  // fused split backward: gdn_bwd_x3w_kernel (one wave per SIMD, pipelined)
+#endif
 #ifndef GDN_DMA_ASM
 #define GDN_DMA_ASM 1
 #endif
@@ -413,11 +416,22 @@ __global__ void __launch_bounds__(768, 1)
 }
 
 // ============================================================== backward
+// Split bf16 planes of the backward ([pixel][channel], C = 192 bf16 per row, no padding): the 8-channel
+// (16-B) chunk k of row m is stored at chunk k ^ pl_sw(m), pl_sw(m) = 4 bit1(m) + 2 bit2(m) (within the
+// row's aligned groups of 8 chunks).  Conflict-free for both readers: the dgamma GEMM's transposed reads
+// (ds_read_b64_tr_b16: 4 consecutive rows x 32 channels per 32 lanes -- rows differ in bank bits 5
+// (row parity, 384-B rows) and 4 (bit 1)) and the split dx GEMM's A fragments (ds_read_b128: row li,
+// chunk 4u + lg -- within each 16-lane bank group of b128 the 16 (row, chunk) pairs cover the 64 banks).
+__device__ __forceinline__ int pl_sw(int m) { return (((m >> 1) & 1) << 2) | (((m >> 2) & 1) << 1); }
+template <int C>
+__device__ __forceinline__ int pl_off(int m, int n) {
+  return m * C + ((((n >> 3) ^ pl_sw(m))) << 3) + (n & 7);
+}
+
 // phase A of one tile (elementwise, identical swizzled offsets in every image):
 // q = dL/dnorm, and the direct term dy*norm^-1/2 (IGDN: dy*norm^1/2) over dy
 // X3: also write q and x^2, split into three bf16 terms, as [pixel][channel]
-// images (sb: q planes then x^2 planes, unpadded C-wide rows whose 16-B chunks
-// are XOR-swizzled by 4 on rows with bit 1 set) for the split dgamma GEMM
+// planes (sb: q planes then x^2 planes, swizzled by pl_off) for the split GEMMs
 // BF: bf16 operands (config C3): only the first plane, q and x^2 rounded to nearest even
 template <int C, int BM, bool X3 = false, bool BF = false>
 __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
@@ -450,7 +464,7 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
     if constexpr (X3) {
       typedef __bf16 b4 __attribute__((ext_vector_type(4)));
       const int m = pos / (C / 4), lc = (pos - m * (C / 4)) ^ (m & 15);
-      const int col = (4 * lc) ^ (((m >> 1) & 1) << 5);
+      const int col = pl_off<C>(m, 4 * lc) - m * C;
       constexpr int PL = BM * C;  // one plane
 #pragma unroll
       for (int op = 0; op < 2; ++op) {
@@ -644,14 +658,15 @@ __global__ void __launch_bounds__(512, 2)
     constexpr int PL = TILE;  // bf16 elements per plane
     const int wq = w - 4, wm2 = wq >> 1, wn2 = wq & 1;
     const int r = lane & 31, h = lane >> 5;
-    // transposed read of rows 8h + (li >> 2) (+4), columns c0 + 16*(lane>>4 & 1) + 4*(li & 3);
-    // rows with bit 1 set store their chunks XOR 32 bf16
-    const int tr_row = (8 * h + (li >> 2)) * C;
+    // transposed read of rows 8h + (li >> 2) (lo) and that + 4 (hi), columns c0 + 16*(lane>>4 & 1) + 4*(li & 3)
+    const int tr_row = 8 * h + (li >> 2);
     const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
-    const int tr_sw = ((li >> 3) & 1) << 5;
-    auto tr8 = [&](const __bf16* src) {
-      const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)src);
-      const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * C));
+    auto tr8 = [&](const __bf16* plane, int c0) {
+      const int c = c0 + tr_col;
+      const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) b4*)(plane + pl_off<C>(tr_row, c)));
+      const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) b4*)(plane + pl_off<C>(tr_row + 4, c)));
       return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
     floatx16 acc[3][3];
@@ -683,12 +698,12 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
       for (int q = 0; q < NP; ++q)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) bb[q][j] = tr8(sbf + NP * PL + q * PL + tr_row + ((96 * wn2 + 32 * j + tr_col) ^ tr_sw));
+        for (int j = 0; j < 3; ++j) bb[q][j] = tr8(sbf + NP * PL + q * PL, 96 * wn2 + 32 * j);
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         b8 a[NP];
 #pragma unroll
-        for (int q = 0; q < NP; ++q) a[q] = tr8(sbf + q * PL + tr_row + ((96 * wm2 + 32 * i + tr_col) ^ tr_sw));
+        for (int q = 0; q < NP; ++q) a[q] = tr8(sbf + q * PL, 96 * wm2 + 32 * i);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           if constexpr (BF) {
@@ -815,6 +830,226 @@ __global__ void __launch_bounds__(512, 2)
 }
 
 
+// ============================================================== backward, whole split, pipelined
+// gdn_bwd_x3w_kernel (C = 192, IC_MATH_SPLIT): both contractions in split arithmetic, one wave per SIMD
+// (4 waves, up to 512 registers each), software-pipelined over 16-pixel tiles with ONE barrier per tile.
+// Wave w owns
+//   * the dx columns k in [48w, 48w+48): gamma's three split planes as MFMA A fragments in 216 VGPRs,
+//     dx^T tile = gamma^T q^T on v_mfma_f32_16x16x32_bf16 (six products), so each lane's results are
+//     4 consecutive channels of one pixel -- the same (pixel li, channels 48w+16j+4lg..+3) elements the
+//     lane loads, runs phase A on and stores: no LDS copy-out, 16-B global loads and stores;
+//   * the 96x96 dgamma quadrant (w>>1, w&1) in 144 accumulators (v_mfma_f32_32x32x16_bf16, K = the
+//     tile's 16 pixels, transposed plane reads), as group B of gdn_bwd_fused_kernel<192, true>.
+// Iteration for tile t (planes / x,dv slots of t in buffer cb, written one iteration earlier):
+//   dx GEMM(t) interleaved with phase A(t+G) (registers -> planes and x,dv slots of buffer cb^1) |
+//   loads of tile t+2G into the landing registers | dgamma GEMM(t) | epilogue(t): dx = dv + 2 x s,
+//   16-B stores | barrier.
+// Global loads are register-staged (the landing registers are free once phase A has consumed them);
+// rows past P load row P-1 with q = dv = 0, and their dx goes to a dump slot (no branches around
+// memory operations, so the compiler's waitcnt pass never waits for the stores).
+// dbeta and the dx column sums (the producing conv's bias gradient) accumulate in per-lane LDS slots.
+template <int C, bool INV>
+__global__ void __launch_bounds__(256, 1)
+    gdn_bwd_x3w_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
+                       const float* __restrict__ gamma, float* __restrict__ dx,
+                       float* __restrict__ slab, uint32_t P) {
+  static_assert(C == 192, "4 waves x 48 dx columns, 2 x 2 dgamma quadrants of 96");
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  constexpr int BM = 16, NT = 256, K32 = C / 32;
+  constexpr int PL = BM * C;      // bf16 elements per plane
+  constexpr int PSET = 6 * PL;    // q planes then x^2 planes
+  __shared__ __attribute__((aligned(16))) __bf16 pls[2 * PSET];      // 72 KB: two plane sets
+  __shared__ __attribute__((aligned(16))) floatx4v xdv[2][6][NT];     // 48 KB: x (j) and dv (3 + j) per lane
+  __shared__ __attribute__((aligned(16))) floatx4v acc_s[6][NT];      // 24 KB: dbeta (j), dx column sums (3 + j)
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const uint32_t ntiles = (P + BM - 1) / BM;
+  const uint32_t G = gridDim.x;
+  uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;  // whole block: before any barrier
+
+  // gamma^T fragments: gx[p][j][s] = plane p of gamma[n = 32s + 8lg + e][k = 48w + 16j + li]
+  b8 gx[3][3][K32];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int s = 0; s < K32; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 hh, mm, ll;
+        split3_bf16(gamma[(size_t)(32 * s + 8 * lg + e) * C + 48 * w + 16 * j + li], hh, mm, ll);
+        gx[0][j][s][e] = hh;
+        gx[1][j][s][e] = mm;
+        gx[2][j][s][e] = ll;
+      }
+  // the 216 gamma registers live in AGPRs (MFMA A operands may be AGPRs): the 256 arch VGPRs of the
+  // wave then hold the dgamma accumulators, the landing registers and phase A
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int s = 0; s < K32; ++s) asm volatile("" : "+a"(gx[p][j][s]));
+#pragma unroll
+  for (int k = 0; k < 6; ++k) acc_s[k][tid] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  // this lane's elements: pixel li of the tile, channels n0(j) = 48w + 16j + 4lg .. +3
+  const int cbase = 48 * w + 4 * lg;
+  floatx4v lx[3], ln[3], ld[3];  // landing registers: x, norm, dy of the next tile to run phase A on
+  auto load = [&](uint32_t t) {
+    const uint32_t m = min(t * BM + li, P - 1);
+    const size_t o = (size_t)m * C + cbase;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      lx[j] = *(const floatx4v*)(x + o + 16 * j);
+      ln[j] = *(const floatx4v*)(norm + o + 16 * j);
+      ld[j] = *(const floatx4v*)(dy + o + 16 * j);
+    }
+  };
+  // phase A, element group j of tile t from the landing registers into buffer b
+  auto phase_a = [&](uint32_t t, int b, int j) {
+    // rows past P (and a tile past the end) contribute nothing: q = dv = 0 by selects (no branch)
+    const bool valid = t < ntiles && t * BM + li < P;
+    const floatx4v xv = lx[j], nv = ln[j], gv = ld[j];
+    floatx4v qv, dv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rs = __builtin_amdgcn_rsqf(nv[e]);
+      const float q = INV ? 0.5f * gv[e] * xv[e] * rs : -0.5f * gv[e] * xv[e] * (rs * rs * rs);
+      const float d = INV ? gv[e] * (nv[e] * rs) : gv[e] * rs;
+      qv[e] = valid ? q : 0.f;
+      dv[e] = valid ? d : 0.f;
+    }
+    __bf16* sp = pls + b * PSET + pl_off<C>(li, cbase + 16 * j);
+    b4 h, m, l;
+    split3_bf16x4(qv, h, m, l);
+    *(b4*)sp = h;
+    *(b4*)(sp + PL) = m;
+    *(b4*)(sp + 2 * PL) = l;
+    split3_bf16x4(xv * xv, h, m, l);
+    *(b4*)(sp + 3 * PL) = h;
+    *(b4*)(sp + 4 * PL) = m;
+    *(b4*)(sp + 5 * PL) = l;
+    xdv[b][j][tid] = xv;
+    xdv[b][3 + j][tid] = dv;
+    acc_s[j][tid] += qv;
+  };
+
+  // dgamma quadrant
+  const int wm2 = w >> 1, wn2 = w & 1;
+  const int tr_row = 8 * (lane >> 5) + (li >> 2);
+  const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (li & 3);
+  auto tr8 = [&](const __bf16* plane, int c0) {
+    const int c = c0 + tr_col;
+    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) b4*)(plane + pl_off<C>(tr_row, c)));
+    const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (__attribute__((address_space(3))) b4*)(plane + pl_off<C>(tr_row + 4, c)));
+    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  floatx16 dg[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dg[i][j][e] = 0.f;
+
+  // prologue: phase A of the first tile, loads of the second
+  load(tile);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) phase_a(tile, 0, j);
+  load(tile + G < ntiles ? tile + G : tile);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  float* const dump = slab + (size_t)gridDim.x * GDN_SLAB(C) + (size_t)blockIdx.x * NT * 4;
+  for (int cb = 0; tile < ntiles; tile += G, cb ^= 1) {
+    const uint32_t nx = tile + G;
+    const __bf16* sp = pls + cb * PSET;
+    // dx^T GEMM(t) (k rows 48w+16j+4lg+r, pixel column li) with phase A(t+G) between its steps
+    floatx4v acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < K32; ++s) {
+      const int off = pl_off<C>(li, 32 * s + 8 * lg);
+      const b8 a0 = *(const b8*)(sp + off), a1 = *(const b8*)(sp + PL + off), a2 = *(const b8*)(sp + 2 * PL + off);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a2, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][s], a1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[2][j][s], a0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][s], a0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a0, acc[j], 0, 0, 0);
+      }
+      if (s & 1) phase_a(nx, cb ^ 1, s >> 1);
+    }
+    // the landing registers are free: loads of tile t+2G (a tile past the end reloads this one)
+    load(tile + 2 * G < ntiles ? tile + 2 * G : tile);
+    // dgamma GEMM(t) on the quadrant
+    b8 av[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) av[i][p] = tr8(sp + p * PL, 96 * wm2 + 32 * i);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      b8 bb[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bb[p] = tr8(sp + (3 + p) * PL, 96 * wn2 + 32 * j);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bb[0], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bb[1], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[2], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bb[0], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[1], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[0], dg[i][j], 0, 0, 0);
+      }
+    }
+    // epilogue(t): dx = dv + 2 x s, stored straight from the registers
+    {
+      const uint32_t m = tile * BM + li;
+      float* dst = m < P ? dx + (size_t)m * C + cbase : dump + tid * 4;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const floatx4v xv = xdv[cb][j][tid], dv = xdv[cb][3 + j][tid];
+        const floatx4v d = dv + 2.f * xv * acc[j];
+        *(floatx4v*)(dst + (m < P ? 16 * j : 0)) = d;
+        acc_s[3 + j][tid] += d;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // partials: dgamma quadrant, then dbeta and the dx column sums summed over the 16 pixels li in order
+  float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      // C/D map of the 32x32 MFMA: row (A index n) = (reg&3) + 8(reg>>2) + 4h, col (B index k) = lane&31
+      const int n = 96 * wm2 + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) out[(size_t)n * C + 96 * wn2 + 32 * j + r] = dg[i][j][reg];
+    }
+  if (tid < 2 * C) {
+    // tid < C: dbeta[tid]; C <= tid < 2C: column sum of channel tid - C.  Channel n lives in lane
+    // (li, lg = (n % 16) / 4) of wave n / 48, slot j = (n % 48) / 16, element n % 4.
+    const int n = tid < C ? tid : tid - C, kind = tid < C ? 0 : 3;
+    const int wv = n / 48, j = (n % 48) / 16, lgn = (n % 16) / 4, e = n % 4;
+    float sum = 0.f;
+    for (int l = 0; l < 16; ++l) sum += acc_s[kind + j][64 * wv + 16 * lgn + l][e];
+    out[C * C + (tid < C ? 0 : C) + n] = sum;
+  }
+}
+
+
 // fixed-order sum of the per-block partials
 // 64 elements x 4 groups of partials per block; each group sums a quarter of
 // the partials with eight loads in flight, the quarters combine in LDS in a
@@ -921,13 +1156,29 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
   }
 }
 
-size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * GDN_SLAB(C) * sizeof(float); }
+// per-block partial slabs, then (gdn_bwd_x3w_kernel) one 4 KB dump slot per block for the dx of rows past P
+size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * (GDN_SLAB(C) + 1024) * sizeof(float); }
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {
   float* slab = (float*)ws;
   if (split == 2 && C == 192)
     return gdn_bwd_fused_launch<192, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
+  if (split && C == 192 && GDN_BWD_X3W) {
+    const int grid = bwd_grid(P);
+    if (grid < 1) return IC_OK;
+    if (inverse)
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, true>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx, slab,
+                         (uint32_t)P);
+    else
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, false>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx, slab,
+                         (uint32_t)P);
+    IC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((GDN_SLAB(192) + 63) / 64), dim3(256), 0, s, slab, grid, 192,
+                       dgamma, dbeta, dxsum);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   if (split && C == 192)
     return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   switch (C) {

@@ -57,21 +57,38 @@ def teardown():
         dist.destroy_process_group()
 
 
-def _joined_allreduce_hook(streams, bucket):
-    """DDP comm hook: the bucket's all-reduce after every stream that produces gradients.
+class _CommState:
+    """State of the comm hook: the streams that produce gradients and a dedicated comm stream."""
 
-    The reducer calls a hook when the last gradient of a bucket is accumulated, on that
-    gradient's stream; RCCL then orders the collective after that stream only.  With the
-    hyperprior on its side stream a bucket can mix gradients finished on both streams, so the
-    current stream first waits for the other one (an event at its tail: everything the
-    autograd engine has queued on it so far, which includes the bucket's own gradients).
-    Then the default hook: divide by the world size, all-reduce (SUM) the bucket in place."""
-    from torch.distributed.algorithms.ddp_comm_hooks.default_hooks import allreduce_hook
-    cur = torch.cuda.current_stream()
-    for s in streams:
-        if s != cur:
-            cur.wait_stream(s)
-    return allreduce_hook(None, bucket)
+    def __init__(self, streams, device):
+        self.streams = list(streams)
+        self.comm = torch.cuda.Stream(device=device)
+        self.world = dist.get_world_size()
+
+
+def _comm_stream_allreduce_hook(state, bucket):
+    """DDP comm hook: each bucket's all-reduce on a dedicated comm stream that waits for every
+    gradient-producing stream; no compute stream ever waits on another here.
+
+    The reducer calls a hook when the last gradient of a bucket has been accumulated, on that
+    gradient's stream.  With the hyperprior on its side stream (and its convs' weight gradients on
+    a third stream) a bucket can mix gradients finished on several streams, so the collective must
+    follow all of them.  The comm stream waits on an event recorded at each producing stream's tail
+    (recording costs the producer nothing: the main, side and weight-gradient streams go on with
+    the backward), then divides the bucket by the world size and all-reduces it (SUM) in place --
+    the default hook's arithmetic, issued under the comm stream, which RCCL's own stream then
+    follows.  DDP's finalize waits for every bucket's future on the stream that ends the backward,
+    and the next step's side-stream work follows that stream, so the gradient views are never
+    rewritten while a collective reads them.  Unmeasured on RCCL hardware (one GPU per box here);
+    tests/test_ddp_gpu.py checks the gradients bitwise with gloo over GPU tensors."""
+    comm = state.comm
+    for s in state.streams:
+        comm.wait_stream(s)
+    buf = bucket.buffer()
+    with torch.cuda.stream(comm):
+        buf.div_(state.world)
+        fut = dist.all_reduce(buf, async_op=True).get_future()
+    return fut.then(lambda f: f.value()[0])
 
 
 def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
@@ -88,7 +105,8 @@ def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
       construction for the model's life; made on the main stream, they would accumulate the
       other streams' gradients there, a cross-stream use of the gradient's memory the caching
       allocator is not told about);
-    * a comm hook (_joined_allreduce_hook) joins every such stream before each bucket's all-reduce.
+    * a comm hook (_comm_stream_allreduce_hook) issues each bucket's all-reduce on a comm stream
+      that waits for every such stream (the compute streams never wait for each other there).
     concurrent=False runs the single-stream step (bitwise the same arithmetic)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return model
@@ -99,17 +117,25 @@ def wrap(model, device, bucket_cap_mb=12.0, concurrent=True):
         model.concurrent_hyperprior = conc
     keep, streams = [], [torch.cuda.current_stream(device)] if conc else []
     if conc:
-        for stream, params in model.gradient_streams(device):
-            streams.append(stream)
-            with torch.cuda.stream(stream):
-                for p in params:
-                    if p.requires_grad:
-                        keep.append(p.view_as(p).grad_fn.next_functions[0][0])  # AccumulateGrad on `stream`
+        # (under enable_grad: a view made under no_grad has no grad_fn).  The nodes must not exist
+        # yet: a node made earlier (by a forward in grad mode whose graph is still alive) would be
+        # returned as it is, on whatever stream it was made -- wrap the model before its first step.
+        with torch.enable_grad():
+            for stream, params in model.gradient_streams(device):
+                streams.append(stream)
+                with torch.cuda.stream(stream):
+                    for p in params:
+                        if p.requires_grad:
+                            gf = p.view_as(p).grad_fn
+                            if gf is None:
+                                raise RuntimeError("distributed.wrap: no AccumulateGrad node for a hyperprior "
+                                                   "parameter")
+                            keep.append(gf.next_functions[0][0])  # AccumulateGrad on `stream`
     ids = [device.index] if device.type == "cuda" else None
     ddp = DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
               broadcast_buffers=False)
     if conc:
-        ddp.register_comm_hook(streams, _joined_allreduce_hook)
+        ddp.register_comm_hook(_CommState(streams, device), _comm_stream_allreduce_hook)
     del keep  # DDP holds the nodes now
     return ddp
 

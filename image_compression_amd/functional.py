@@ -336,6 +336,9 @@ class _ConvWGradFn(Function):
         pre = _take_colsum(gz) if (ctx.has_b and not act) else None  # bias gradient formed by gz's producer
         if pre is not None:
             pre.record_stream(cur)
+        if act:
+            # the fused-ReLU output was allocated on the producing (side) stream and is read here
+            ctx.holder["y"].record_stream(cur)
         gy = relu_bwd(ctx.holder["y"], gz) if act else gz
         gy = _cl(gy)
         ops, k = _lib.ops(), w.shape[2]

@@ -111,7 +111,22 @@ class Compressor2018(nn.Module):
                 for m, v in zip(mods, vals):
                     m.__dict__["_pre"] = v
 
+    def _clear_reparameterised(self):
+        from ..layers.gdn import NonNegativeParam
+        for blk in (self.analysis_transform, self.synthesis_transform):
+            for m in blk.modules():
+                if isinstance(m, NonNegativeParam):
+                    m.__dict__.pop("_pre", None)
+
     def forward(self, x):
+        # every GDN consumes its pre-formed value during the step; if the step raises first, none
+        # may stay behind in the module (a stale value, and a graph kept alive by module state)
+        try:
+            return self._forward(x)
+        finally:
+            self._clear_reparameterised()
+
+    def _forward(self, x):
         if self.training:
             _noise.begin_step(x.device)  # fresh Philox counters for this step
         self._reparameterise_gdn(x)

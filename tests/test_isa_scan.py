@@ -1,9 +1,10 @@
 """The built library's gfx950 code objects carry no packed-fp32 VALU instruction
-(v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32), whose result a following instruction read stale
-when MFMA kernels shared the SIMD (the round-3 fact_bwd_k fault; tools/pk_hazard_probe.hip
-reproduces it in isolation).  Every source is built with -packed-fp32-ops disabled (csrc/Makefile);
-this scan catches a source, flag or inline asm that reintroduces one.  CPU only: it disassembles
-the in-tree libimgcomp.so (tools/isa_scan.py)."""
+(v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32).  The round-3 fact_bwd_k fault -- wrong w1 / w2 gradient
+sums in concurrent model steps, only in builds with packed-fp32 instructions -- is mitigated by
+building every source without them (what is and is not established; the
+isolated probes, tools/pk_hazard_probe.hip among them, did NOT reproduce it).  This scan catches a
+source, flag or inline asm that reintroduces one.  CPU only: it disassembles the in-tree
+libimgcomp.so (tools/isa_scan.py)."""
 import importlib.util
 import os
 

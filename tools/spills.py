@@ -14,11 +14,14 @@ import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "image_compression_amd", "csrc")
+# extra hipcc flags (e.g. -DGDN_BWD_XD=0) from the environment; the Makefile's no-packed-fp32 flag is always on
+EXTRA = os.environ.get("SPILLS_FLAGS", "").split()
 
 
 def analyse(src):
     with tempfile.TemporaryDirectory() as td:
-        r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", CSRC, "-c", src,
+        r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", CSRC, *EXTRA,
+                            "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-c", src,
                             "-o", os.path.join(td, "x.o"), "-Rpass-analysis=kernel-resource-usage"],
                            capture_output=True, text=True)
     out, cur = [], None
