@@ -56,6 +56,16 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef GDN_BWD_X3W
 #define GDN_BWD_X3W 1  // fused split backward: gdn_bwd_x3w_kernel (one wave per SIMD, pipelined)
 #endif
+#ifndef X3W_ABL
+#define X3W_ABL 0  // diagnostic ablations of gdn_bwd_x3w_kernel (wrong results): 1 no loads in the loop, 2 no
+                   // phase A, 4 no dgamma MFMAs, 8 no dx MFMAs, 16 no dx stores
+#endif
+#ifndef X3W_STAMP
+#define X3W_STAMP 0  // diagnostic: per-iteration s_memtime stamps of gdn_bwd_x3w_kernel into the workspace
+#endif
+#ifndef X3W_SGB
+#define X3W_SGB 1  // gdn_bwd_x3w_kernel: interleave phase A / epilogue with the MFMAs (sched_group_barrier)
+#endif
 #ifndef GDN_DMA_ASM
 #define GDN_DMA_ASM 1
 #endif
@@ -417,12 +427,15 @@ __global__ void __launch_bounds__(768, 1)
 
 // ============================================================== backward
 // Split bf16 planes of the backward ([pixel][channel], C = 192 bf16 per row, no padding): the 8-channel
-// (16-B) chunk k of row m is stored at chunk k ^ pl_sw(m), pl_sw(m) = 4 bit1(m) + 2 bit2(m) (within the
-// row's aligned groups of 8 chunks).  Conflict-free for both readers: the dgamma GEMM's transposed reads
-// (ds_read_b64_tr_b16: 4 consecutive rows x 32 channels per 32 lanes -- rows differ in bank bits 5
-// (row parity, 384-B rows) and 4 (bit 1)) and the split dx GEMM's A fragments (ds_read_b128: row li,
-// chunk 4u + lg -- within each 16-lane bank group of b128 the 16 (row, chunk) pairs cover the 64 banks).
-__device__ __forceinline__ int pl_sw(int m) { return (((m >> 1) & 1) << 2) | (((m >> 2) & 1) << 1); }
+// (16-B) chunk k of row m (0..15) is stored at chunk k ^ pl_sw(m), pl_sw(m) = 4 bit1(m) + ((4 - (m>>2)) & 3)
+// (within the row's aligned groups of 8 chunks).  Conflict-free for both readers: the dgamma GEMM's
+// transposed reads (ds_read_b64_tr_b16: 4 consecutive rows x 32 channels per 32 lanes -- the rows differ
+// in bank bits 5 (row parity, 384-B rows) and 4 (bit 1)) and the split dx GEMM's fragments (ds_read_b128:
+// row li, chunk 4u + lg -- within each 16-lane bank group of b128 the 16 (row, chunk) pairs cover the 64
+// banks); the phase-A stores of gdn_bwd_x3w_kernel (ds_write_b64, 16 rows of one channel group per 16
+// lanes) are 2-way, the least any chunk-granular swizzle of 384-B rows allows (was 4-way with
+// 4 bit1 + 2 bit2; bank simulation: tools/plane_banks.py).
+__device__ __forceinline__ int pl_sw(int m) { return (((m >> 1) & 1) << 2) | ((4 - (m >> 2)) & 3); }
 template <int C>
 __device__ __forceinline__ int pl_off(int m, int n) {
   return m * C + ((((n >> 3) ^ pl_sw(m))) << 3) + (n & 7);
@@ -908,6 +921,12 @@ __global__ void __launch_bounds__(256, 1)
       ld[j] = *(const floatx4v*)(dy + o + 16 * j);
     }
   };
+  auto load_j = [&](uint32_t t, int j) {
+    const size_t o = (size_t)min(t * BM + li, P - 1) * C + cbase + 16 * j;
+    lx[j] = *(const floatx4v*)(x + o);
+    ln[j] = *(const floatx4v*)(norm + o);
+    ld[j] = *(const floatx4v*)(dy + o);
+  };
   // phase A, element group j of tile t from the landing registers into buffer b
   auto phase_a = [&](uint32_t t, int b, int j) {
     // rows past P (and a tile past the end) contribute nothing: q = dv = 0 by selects (no branch)
@@ -966,66 +985,157 @@ __global__ void __launch_bounds__(256, 1)
   __builtin_amdgcn_s_barrier();
 
   float* const dump = slab + (size_t)gridDim.x * GDN_SLAB(C) + (size_t)blockIdx.x * NT * 4;
+#if X3W_STAMP
+  // diagnostic build: s_memtime at four points of each of the first 160 iterations, per wave
+  uint64_t* const stp = (uint64_t*)(slab + (size_t)gridDim.x * (GDN_SLAB(C) + 1024)) +
+                        ((size_t)blockIdx.x * 4 + w) * 160 * 4;
+  int it = 0;
+#define X3W_ST(k) \
+  if (lane == 0 && it < 160) stp[it * 4 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define X3W_ST(k)
+#endif
   for (int cb = 0; tile < ntiles; tile += G, cb ^= 1) {
+    X3W_ST(0)
     const uint32_t nx = tile + G;
+    const uint32_t n2 = tile + 2 * G < ntiles ? tile + 2 * G : tile;  // past the end: reload this tile
     const __bf16* sp = pls + cb * PSET;
-    // dx^T GEMM(t) (k rows 48w+16j+4lg+r, pixel column li) with phase A(t+G) between its steps
+    // dx^T GEMM(t) (k rows 48w+16j+4lg+r, pixel column li), six K steps of 32 channels; phase A(t+G)
+    // part j and the loads of part j of tile t+2G run between the MFMAs of steps 2j and 2j+1
+    // (one wave per SIMD: the VALU and memory instructions issue in the MFMAs' shadow only when
+    // interleaved with them, sched_group_barrier below)
     floatx4v acc[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    auto qfrag = [&](int st, b8 (&f)[3]) {
+      const int off = pl_off<C>(li, 32 * st + 8 * lg);
+      f[0] = *(const b8*)(sp + off);
+      f[1] = *(const b8*)(sp + PL + off);
+      f[2] = *(const b8*)(sp + 2 * PL + off);
+    };
+    b8 fa[3], fb[3];
+    b8 av[3][3], bb[2][3];  // dgamma GEMM fragments (read during the dx GEMM's last K step)
+    qfrag(0, fa);
+    // phase A(t+G) part pr in six slices, one between each (K step, column tile) group of six MFMAs
+    floatx4v pq, pd, pxv;
+    auto pa_slice = [&](int pr, int k) {
+      if (X3W_ABL & 2) return;
+      const bool valid = nx < ntiles && nx * BM + li < P;
+      __bf16* pp = pls + (cb ^ 1) * PSET + pl_off<C>(li, cbase + 16 * pr);
+      if (k < 2) {  // elements 2k, 2k+1: q, dv
+        if (k == 0) pxv = lx[pr];
 #pragma unroll
-    for (int s = 0; s < K32; ++s) {
-      const int off = pl_off<C>(li, 32 * s + 8 * lg);
-      const b8 a0 = *(const b8*)(sp + off), a1 = *(const b8*)(sp + PL + off), a2 = *(const b8*)(sp + 2 * PL + off);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a2, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][s], a1, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[2][j][s], a0, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a1, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][s], a0, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][s], a0, acc[j], 0, 0, 0);
+        for (int e = 2 * k; e < 2 * k + 2; ++e) {
+          const float xv = lx[pr][e], nv = ln[pr][e], gv = ld[pr][e];
+          const float rs = __builtin_amdgcn_rsqf(nv);
+          const float q = INV ? 0.5f * gv * xv * rs : -0.5f * gv * xv * (rs * rs * rs);
+          const float d = INV ? gv * (nv * rs) : gv * rs;
+          pq[e] = valid ? q : 0.f;
+          pd[e] = valid ? d : 0.f;
+        }
+      } else if (k == 2) {  // q's split planes
+        b4 h, m, l;
+        split3_bf16x4(pq, h, m, l);
+        *(b4*)pp = h;
+        *(b4*)(pp + PL) = m;
+        *(b4*)(pp + 2 * PL) = l;
+      } else if (k == 3) {  // x^2's split planes
+        b4 h, m, l;
+        split3_bf16x4(pxv * pxv, h, m, l);
+        *(b4*)(pp + 3 * PL) = h;
+        *(b4*)(pp + 4 * PL) = m;
+        *(b4*)(pp + 5 * PL) = l;
+      } else if (k == 4) {
+        xdv[cb ^ 1][pr][tid] = pxv;
+        xdv[cb ^ 1][3 + pr][tid] = pd;
+        acc_s[pr][tid] += pq;
+      } else if (!(X3W_ABL & 1)) {  // the landing registers of part pr are free: tile t+2G's
+        load_j(n2, pr);
       }
-      if (s & 1) phase_a(nx, cb ^ 1, s >> 1);
+    };
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int pr = 0; pr < K32 / 2; ++pr) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int st = 2 * pr + h2;
+        b8 (&cur)[3] = h2 ? fb : fa;
+        b8 (&nxt)[3] = h2 ? fa : fb;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j == 0 && st + 1 < K32) qfrag(st + 1, nxt);
+          if (!(X3W_ABL & 8)) {
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[2], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][st], cur[1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[2][j][st], cur[0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][st], cur[0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[0], acc[j], 0, 0, 0);
+          }
+          pa_slice(pr, 3 * h2 + j);
+          if (X3W_SGB) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
-    // the landing registers are free: loads of tile t+2G (a tile past the end reloads this one)
-    load(tile + 2 * G < ntiles ? tile + 2 * G : tile);
-    // dgamma GEMM(t) on the quadrant
-    b8 av[3][3];
+    X3W_ST(1)
+    // dgamma GEMM(t) on the quadrant, with the epilogue of tile t (dx = dv + 2 x s, stored straight
+    // from the registers) between its MFMAs
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int p = 0; p < 3; ++p) av[i][p] = tr8(sp + p * PL, 96 * wm2 + 32 * i);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      b8 bb[3];
+    for (int p = 0; p < 3; ++p) bb[0][p] = tr8(sp + (3 + p) * PL, 96 * wn2);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bb[p] = tr8(sp + (3 + p) * PL, 96 * wn2 + 32 * j);
+    for (int j = 0; j < 3; ++j) {
+      if (j + 1 < 3)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bb[(j + 1) & 1][p] = tr8(sp + (3 + p) * PL, 96 * wn2 + 32 * (j + 1));
+      const b8 (&bc)[3] = bb[j & 1];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bb[0], dg[i][j], 0, 0, 0);
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bb[1], dg[i][j], 0, 0, 0);
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[2], dg[i][j], 0, 0, 0);
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bb[0], dg[i][j], 0, 0, 0);
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[1], dg[i][j], 0, 0, 0);
-        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bb[0], dg[i][j], 0, 0, 0);
+        if (X3W_ABL & 4) continue;
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bc[0], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bc[1], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[2], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bc[0], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[1], dg[i][j], 0, 0, 0);
+        dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[0], dg[i][j], 0, 0, 0);
       }
-    }
-    // epilogue(t): dx = dv + 2 x s, stored straight from the registers
-    {
-      const uint32_t m = tile * BM + li;
-      float* dst = m < P ? dx + (size_t)m * C + cbase : dump + tid * 4;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      {  // epilogue, element group j
+        const uint32_t m = tile * BM + li;
+        float* dst = m < P ? dx + (size_t)m * C + cbase + 16 * j : dump + tid * 4;
         const floatx4v xv = xdv[cb][j][tid], dv = xdv[cb][3 + j][tid];
         const floatx4v d = dv + 2.f * xv * acc[j];
-        *(floatx4v*)(dst + (m < P ? 16 * j : 0)) = d;
+        if (!(X3W_ABL & 16)) *(floatx4v*)dst = d;
         acc_s[3 + j][tid] += d;
       }
+      if (X3W_SGB) {
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (k < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (the next bb)
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
+    X3W_ST(2)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    X3W_ST(3)
+#if X3W_STAMP
+    ++it;
+#endif
   }
+#undef X3W_ST
   // partials: dgamma quadrant, then dbeta and the dx column sums summed over the 16 pixels li in order
   float* out = slab + (size_t)blockIdx.x * GDN_SLAB(C);
   const int r = lane & 31, h = lane >> 5;
@@ -1038,14 +1148,14 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
       for (int j = 0; j < 3; ++j) out[(size_t)n * C + 96 * wn2 + 32 * j + r] = dg[i][j][reg];
     }
-  if (tid < 2 * C) {
-    // tid < C: dbeta[tid]; C <= tid < 2C: column sum of channel tid - C.  Channel n lives in lane
+  for (int k = tid; k < 2 * C; k += NT) {
+    // k < C: dbeta[k]; C <= k < 2C: column sum of channel k - C.  Channel n lives in lane
     // (li, lg = (n % 16) / 4) of wave n / 48, slot j = (n % 48) / 16, element n % 4.
-    const int n = tid < C ? tid : tid - C, kind = tid < C ? 0 : 3;
+    const int n = k < C ? k : k - C, kind = k < C ? 0 : 3;
     const int wv = n / 48, j = (n % 48) / 16, lgn = (n % 16) / 4, e = n % 4;
     float sum = 0.f;
     for (int l = 0; l < 16; ++l) sum += acc_s[kind + j][64 * wv + 16 * lgn + l][e];
-    out[C * C + (tid < C ? 0 : C) + n] = sum;
+    out[C * C + k] = sum;
   }
 }
 
@@ -1157,7 +1267,9 @@ int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inv
 }
 
 // per-block partial slabs, then (gdn_bwd_x3w_kernel) one 4 KB dump slot per block for the dx of rows past P
-size_t gdn_bwd_fused_ws(int C, long long P) { return (size_t)bwd_grid(P) * (GDN_SLAB(C) + 1024) * sizeof(float); }
+size_t gdn_bwd_fused_ws(int C, long long P) {
+  return (size_t)bwd_grid(P) * (GDN_SLAB(C) + 1024) * sizeof(float) + (X3W_STAMP ? (size_t)256 * 4 * 160 * 4 * 8 : 0);
+}
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {

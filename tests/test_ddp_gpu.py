@@ -2,8 +2,8 @@
 tensors, sharing the box's one GPU — the RCCL path needs one GPU per rank),
 each on half the batch, average to the single-process gradient of the whole
 batch (injected noise, fixed weights) -- under DistributedDataParallel with the
-hyperprior side stream (D.wrap's comm hook joins both streams before each bucket's
-all-reduce; bitwise equal to the single-stream DDP step) and through TrainStep's flat
+hyperprior side stream (D.wrap's comm hook issues each bucket's all-reduce on a comm
+stream that waits for every gradient-producing stream; bitwise equal to the single-stream DDP step) and through TrainStep's flat
 gradient buffer and one all-reduce.  The ranks'
 training-noise keys differ (noise.rank_key).  Unmeasured on RCCL hardware:
 the box has one GPU."""

@@ -15,7 +15,7 @@ NOPK_SRCS=${NOPK_SRCS-"igemm wgrad pack conv_api gdn elementwise entropy msssim 
 for f in igemm wgrad pack conv_api gdn elementwise entropy msssim im2col gdn_fused edge optim metrics; do
   extra=""
   case " $NOPK_SRCS " in *" $f "*) extra="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
-  [ $f = gdn_fused ] && extra="$extra -mllvm -amdgpu-mfma-vgpr-form"  # as the Makefile (FLAGS_gdn_fused)
+  [ $f = gdn_fused ] && extra="$extra -mllvm -amdgpu-mfma-vgpr-form $GDN_FLAGS"  # as the Makefile (FLAGS_gdn_fused); GDN_FLAGS: extra flags for this file only
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C $extra "$@" -c $C/$f.hip -o $B/$f.o 2>&1 \
     | grep -v "not a recognized feature" &
 done

@@ -12,5 +12,10 @@ timeout -k 10 120 python tools/gdn_bwd_time.py > gpurun_out/gdntime_$TAG.txt 2>&
 IMGCOMP_LIB=$R/tools/_abl/$ABL/libimgcomp.so timeout -k 10 120 python tools/gdn_bwd_time.py >> gpurun_out/gdntime_$TAG.txt 2>&1 || { echo TIME2 FAIL; exit 1; }
 timeout -k 10 120 python tools/gdn_bwd_time.py >> gpurun_out/gdntime_$TAG.txt 2>&1 || { echo TIME3 FAIL; exit 1; }
 grep -v amdgpu.ids gpurun_out/gdntime_$TAG.txt
+if [ -n "$FULL" ]; then
+  timeout -k 10 900 python -u -m pytest -q -p no:cacheprovider --timeout 300 --timeout-method thread tests -m gpu \
+    > gpurun_out/gputests_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/gputests_$TAG.log
+  [ $rc -eq 0 ] || { echo "FULL TESTS rc=$rc"; grep -E "^FAILED|Error" gpurun_out/gputests_$TAG.log | head; exit 1; }
+fi
 [ $# -gt 0 ] && bash tools/gpu_cfgprof.sh $TAG "$@"
 echo DONE
