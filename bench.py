@@ -305,6 +305,9 @@ def main():
                          "with the backward, never a graph replay followed by an unbucketed all-reduce.")
     ap.add_argument("--math", default=None, choices=["fp32", "fp32_split", "bf16"],
                     help="override the config's cfg.MODEL.COMPUTE_DTYPE")
+    ap.add_argument("--serial-hyperprior", action="store_true",
+                    help="run the hyperprior branch on the main stream (Compressor2018.concurrent_hyperprior "
+                         "= False; bitwise the same arithmetic)")
     args = ap.parse_args()
     conf = dict(CONFIGS[args.config])
     if args.math:
@@ -321,6 +324,8 @@ def main():
     from image_compression_amd.step import TrainStep
     torch.manual_seed(0)
     model = modelling.build_model(_cfg(conf=conf)).to(dev).train()
+    if args.serial_hyperprior:
+        model.concurrent_hyperprior = False
     # each rank draws its own shard of the synthetic global batch (weak scaling)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, args.size, args.size, device=dev, generator=g)
@@ -332,7 +337,8 @@ def main():
             _, losses = model(x)
             losses["total_loss"].backward()
             return losses
-        mode = "eager, DDP 12 MB buckets" if dist else "eager"
+        mode = ("eager, DDP 12 MB buckets" if dist else "eager") + (
+            ", hyperprior on the main stream" if args.serial_hyperprior else ", hyperprior on a side stream")
     else:
         # fwd + loss + bwd captured once into a hipGraph and replayed (one GPU)
         step = TrainStep(model, x, graph=True)

@@ -339,6 +339,184 @@ __global__ void scale_out_k(const float* ga, const float* gb, long long n, float
   }
 }
 
+// ---------------------------------------------------------------- fused tile kernels (filter size 11)
+// One block per (tile, plane) does a level's whole separable filtering in LDS, so the five filtered
+// moment images (and in the backward the five derivative maps and their vertical adjoint) never go
+// to HBM: the forward reads a and b once per level, the backward reads a, b and the level's gradient
+// once and writes the gradient once.  The naive chain (hfilt -> vstats; hfilt -> dmaps -> vadj -> hadj)
+// wrote and re-read 5 moment planes two to three times per level (C4 level 0: 63 MB each).
+#ifndef MSSSIM_FUSED
+#define MSSSIM_FUSED 1
+#endif
+constexpr int FMAX = 11;                      // fused kernels: filter size 11 (every reference config)
+constexpr int FTW = 64, FTH = 16;             // forward: valid outputs per tile
+constexpr int FRW = FTW + FMAX - 1, FRH = FTH + FMAX - 1;
+constexpr int BTW = 32, BTH = 16;             // backward: gradient pixels per tile
+constexpr int BDW = BTW + FMAX - 1, BDH = BTH + FMAX - 1;          // derivative-map region
+constexpr int BIW = BTW + 2 * (FMAX - 1), BIH = BTH + 2 * (FMAX - 1);  // input region
+
+// forward: per tile of FTW x FTH valid outputs, the per-plane partial sums of the cs and ssim maps
+// (part[p][tile][2], summed per plane in a fixed order by vstats_final_k)
+// FS (the filter size) is a template constant: fully unrolled taps, the weights in SGPRs
+template <int FS>
+__global__ void __launch_bounds__(256) ssim_fwd_tile_k(const float* __restrict__ a, const float* __restrict__ b,
+                                                       int H, int W, const Filt f, float c1, float c2,
+                                                       float* __restrict__ part) {
+  __shared__ float A[FRH][FRW], B[FRH][FRW];
+  __shared__ float HM[5][FRH][FTW];
+  __shared__ float red[32];
+  constexpr int fs = FS;
+  static_assert(FS <= FMAX, "LDS regions sized for FMAX");
+  const int Wv = W - fs + 1, Hv = H - fs + 1;
+  const int p = blockIdx.z;
+  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
+  const int tid = threadIdx.x;
+  const float* pa = a + (long long)p * H * W;
+  const float* pb = b + (long long)p * H * W;
+  const int rw = min(FTW, Wv - x0) + fs - 1, rh = min(FTH, Hv - y0) + fs - 1;
+  for (int i = tid; i < FRH * FRW; i += 256) {
+    const int r = i / FRW, c = i - (i / FRW) * FRW;
+    const bool in = r < rh && c < rw;
+    const long long o = (long long)(y0 + r) * W + x0 + c;
+    A[r][c] = in ? pa[o] : 0.f;
+    B[r][c] = in ? pb[o] : 0.f;
+  }
+  __syncthreads();
+  // horizontal pass: HM[q][r][c] = sum_k g[k] m_q(r, c + k)
+  for (int i = tid; i < FRH * FTW; i += 256) {
+    const int r = i / FTW, c = i - (i / FTW) * FTW;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+      const float g = f.g[k], va = A[r][c + k], vb = B[r][c + k];
+      s0 += g * va; s1 += g * vb; s2 += g * (va * va); s3 += g * (vb * vb); s4 += g * (va * vb);
+    }
+    HM[0][r][c] = s0; HM[1][r][c] = s1; HM[2][r][c] = s2; HM[3][r][c] = s3; HM[4][r][c] = s4;
+  }
+  __syncthreads();
+  float v0 = 0.f, v1 = 0.f;
+  for (int i = tid; i < FTH * FTW; i += 256) {
+    const int r = i / FTW, c = i - (i / FTW) * FTW;
+    if (y0 + r >= Hv || x0 + c >= Wv) continue;
+    float ma = 0.f, mb = 0.f, saa = 0.f, sbb = 0.f, sab = 0.f;
+    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+      const float g = f.g[k];
+      ma += g * HM[0][r + k][c]; mb += g * HM[1][r + k][c]; saa += g * HM[2][r + k][c];
+      sbb += g * HM[3][r + k][c]; sab += g * HM[4][r + k][c];
+    }
+    const float mu12 = ma * mb;
+    const float s1 = saa - ma * ma, s2 = sbb - mb * mb, s12 = sab - mu12;
+    const float cs = (2.f * s12 + c2) / (s1 + s2 + c2);
+    v0 += cs;
+    v1 += cs * (2.f * mu12 + c1) / (ma * ma + mb * mb + c1);
+  }
+  float v[2] = {v0, v1};
+  block_sum<2>(v, red);
+  if (tid == 0) {
+    const long long t = (long long)p * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
+    part[t * 2] = v[0];
+    part[t * 2 + 1] = v[1];
+  }
+}
+
+// backward: per tile of BTW x BTH pixels of a level, the gradient contribution of that level's map
+// sums (coef_l = dLoss / d(per-pixel cs, ssim) for each image), accumulated into (ga, gb).
+//   D (five maps) at the valid outputs whose windows reach the tile, from the moments recomputed
+//   there; E = vertical adjoint of D on the tile rows; the horizontal adjoint and the moments' chain
+//   rule onto the tile pixels (as dmaps_k -> vadj_k -> hadj_k)
+template <int FS>
+__global__ void __launch_bounds__(256) ssim_bwd_tile_k(const float* __restrict__ a, const float* __restrict__ b,
+                                                       int C, int H, int W, const Filt f, float c1, float c2,
+                                                       const float* __restrict__ coef_l, float* __restrict__ ga,
+                                                       float* __restrict__ gb) {
+  __shared__ float A[BIH][BIW], B[BIH][BIW];
+  __shared__ float HM[5][BIH][BDW];  // horizontal moments; then E[5][BTH][BDW] in its first rows
+  __shared__ float D[4][BDH][BDW];   // d/d(ma, mb, saa = sbb, sab)
+  constexpr int fs = FS, h = FS - 1;
+  static_assert(FS <= FMAX, "LDS regions sized for FMAX");
+  const int Wv = W - fs + 1, Hv = H - fs + 1;
+  const int p = blockIdx.z, n = p / C;
+  const int x0 = blockIdx.x * BTW, y0 = blockIdx.y * BTH;
+  const int ox = x0 - h, oy = y0 - h;  // origin of the input and D regions
+  constexpr int iw = BTW + 2 * h, ih = BTH + 2 * h, dw = BTW + h, dh = BTH + h;
+  const int tid = threadIdx.x;
+  const float* pa = a + (long long)p * H * W;
+  const float* pb = b + (long long)p * H * W;
+  const float gC = coef_l[n * 2], gS = coef_l[n * 2 + 1];
+  for (int i = tid; i < ih * iw; i += 256) {
+    const int r = i / iw, c = i - (i / iw) * iw;
+    const int y = oy + r, x = ox + c;
+    const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const long long o = (long long)y * W + x;
+    A[r][c] = in ? pa[o] : 0.f;
+    B[r][c] = in ? pb[o] : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < ih * dw; i += 256) {
+    const int r = i / dw, c = i - (i / dw) * dw;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+      const float g = f.g[k], va = A[r][c + k], vb = B[r][c + k];
+      s0 += g * va; s1 += g * vb; s2 += g * (va * va); s3 += g * (vb * vb); s4 += g * (va * vb);
+    }
+    HM[0][r][c] = s0; HM[1][r][c] = s1; HM[2][r][c] = s2; HM[3][r][c] = s3; HM[4][r][c] = s4;
+  }
+  __syncthreads();
+  for (int i = tid; i < dh * dw; i += 256) {
+    const int r = i / dw, c = i - (i / dw) * dw;
+    const int yv = oy + r, xv = ox + c;
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d4 = 0.f;
+    if ((unsigned)yv < (unsigned)Hv && (unsigned)xv < (unsigned)Wv) {
+      float ma = 0.f, mb = 0.f, saa = 0.f, sbb = 0.f, sab = 0.f;
+      _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+        const float g = f.g[k];
+        ma += g * HM[0][r + k][c]; mb += g * HM[1][r + k][c]; saa += g * HM[2][r + k][c];
+        sbb += g * HM[3][r + k][c]; sab += g * HM[4][r + k][c];
+      }
+      const float A1 = 2.f * ma * mb + c1, B1 = ma * ma + mb * mb + c1;
+      const float A2 = 2.f * (sab - ma * mb) + c2;
+      const float B2 = (saa - ma * ma) + (sbb - mb * mb) + c2;
+      const float cs = A2 / B2, lum = A1 / B1;
+      const float ucs = gC + gS * lum, ul = gS * cs;
+      const float gA2 = ucs / B2, gB2 = -ucs * A2 / (B2 * B2);
+      const float gA1 = ul / B1, gB1 = -ul * A1 / (B1 * B1);
+      d0 = -2.f * mb * gA2 - 2.f * ma * gB2 + 2.f * mb * gA1 + 2.f * ma * gB1;
+      d1 = -2.f * ma * gA2 - 2.f * mb * gB2 + 2.f * ma * gA1 + 2.f * mb * gB1;
+      d2 = gB2;
+      d4 = 2.f * gA2;
+    }
+    D[0][r][c] = d0; D[1][r][c] = d1; D[2][r][c] = d2; D[3][r][c] = d4;
+  }
+  __syncthreads();
+  // vertical adjoint onto the tile rows: E[q][y][c] = sum_k g[k] D[q][y + h - k][c]  (E over HM)
+  float (*E)[BIH][BDW] = HM;
+  for (int i = tid; i < BTH * dw; i += 256) {
+    const int y = i / dw, c = i - (i / dw) * dw;
+    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e4 = 0.f;
+    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+      const float g = f.g[k];
+      const int r = y + h - k;
+      e0 += g * D[0][r][c]; e1 += g * D[1][r][c]; e2 += g * D[2][r][c]; e4 += g * D[3][r][c];
+    }
+    E[0][y][c] = e0; E[1][y][c] = e1; E[2][y][c] = e2; E[3][y][c] = e4;
+  }
+  __syncthreads();
+  // horizontal adjoint and the moments' chain rule (hadj_k): s_q[y][x] = sum_k g[k] E[q][y][x + h - k]
+  for (int i = tid; i < BTH * BTW; i += 256) {
+    const int y = i / BTW, x = i - (i / BTW) * BTW;
+    if (y0 + y >= H || x0 + x >= W) continue;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s4 = 0.f;
+    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+      const float g = f.g[k];
+      const int c = x + h - k;
+      s0 += g * E[0][y][c]; s1 += g * E[1][y][c]; s2 += g * E[2][y][c]; s4 += g * E[3][y][c];
+    }
+    const float va = A[y + h][x + h], vb = B[y + h][x + h];
+    const long long o = (long long)p * H * W + (long long)(y0 + y) * W + x0 + x;
+    ga[o] += s0 + 2.f * va * s2 + vb * s4;
+    gb[o] += s1 + 2.f * vb * s2 + va * s4;
+  }
+}
+
 int vstats_blocks(int Hv, int Wv) {
   long long n = (long long)Hv * Wv;
   long long b = (n + 255) / 256;
@@ -347,18 +525,34 @@ int vstats_blocks(int Hv, int Wv) {
   return (int)b;
 }
 
+bool fused_ok(const Geo& g) { return MSSSIM_FUSED && g.fs == FMAX; }
+
+// forward tiles per plane of level l (fused path)
+int fwd_tiles(const Geo& g, int l, int& tx, int& ty) {
+  tx = (g.W[l] - g.fs + 1 + FTW - 1) / FTW;
+  ty = (g.H[l] - g.fs + 1 + FTH - 1) / FTH;
+  return tx * ty;
+}
+
 size_t fwd_ws_bytes(const Geo& g) {
-  // th (5 planes at the largest level) + stats partials
+  // th (5 planes at the largest level; naive path only) + stats partials (per plane: <= 64 blocks of
+  // vstats_k, or one per forward tile)
   const long long Wv = g.W[0] - g.fs + 1;
-  size_t th = (size_t)5 * g.P * g.H[0] * Wv * 4;
-  size_t part = (size_t)g.P * 64 * 2 * 4;
+  size_t th = fused_ok(g) ? 0 : (size_t)5 * g.P * g.H[0] * Wv * 4;
+  int nb = 64;
+  if (fused_ok(g))
+    for (int l = 0; l < g.nlev; ++l) {
+      int tx, ty;
+      nb = max(nb, fwd_tiles(g, l, tx, ty));
+    }
+  size_t part = (size_t)g.P * nb * 2 * 4;
   return ic_align(th, 256) + ic_align(part, 256);
 }
 
 size_t bwd_ws_bytes(const Geo& g) {
   const long long Wv = g.W[0] - g.fs + 1, Hv = g.H[0] - g.fs + 1;
-  size_t th = (size_t)5 * g.P * g.H[0] * Wv * 4;
-  size_t D = (size_t)5 * g.P * Hv * Wv * 4;
+  size_t th = fused_ok(g) ? 0 : (size_t)5 * g.P * g.H[0] * Wv * 4;
+  size_t D = fused_ok(g) ? 0 : (size_t)5 * g.P * Hv * Wv * 4;
   size_t E = th;
   size_t grads = 0;
   for (int l = 0; l < g.nlev; ++l) grads += (size_t)2 * g.P * g.H[l] * g.W[l] * 4;
@@ -404,7 +598,7 @@ int ic_msssim_fwd(const float* a, const float* b, int N, int C, int H, int W, in
   const float c1 = (k1 * max_val) * (k1 * max_val), c2 = (k2 * max_val) * (k2 * max_val);
   char* wsb = (char*)ws;
   float* th = (float*)wsb;
-  float* part = (float*)(wsb + ic_align((size_t)5 * g.P * g.H[0] * (g.W[0] - g.fs + 1) * 4, 256));
+  float* part = (float*)(wsb + (fused_ok(g) ? 0 : ic_align((size_t)5 * g.P * g.H[0] * (g.W[0] - g.fs + 1) * 4, 256)));
   const long long n0 = (long long)g.P * H * W;
   hipLaunchKernelGGL(scale_copy_k, dim3(grid_for(n0)), dim3(256), 0, s, a, b, n0, max_val, state + g.off[0],
                      state + g.off[0] + n0);
@@ -422,12 +616,20 @@ int ic_msssim_fwd(const float* a, const float* b, int N, int C, int H, int W, in
       IC_CHECK_LAUNCH();
       (void)np;
     }
-    const long long nhf = (long long)g.P * Hl * (Wl - g.fs + 1);
-    hipLaunchKernelGGL(hfilt_k, dim3(grid_for(nhf)), dim3(256), 0, s, al, bl, g.P, Hl, Wl, f, th);
-    IC_CHECK_LAUNCH();
-    const int nb = vstats_blocks(Hl - g.fs + 1, Wl - g.fs + 1);
-    hipLaunchKernelGGL(vstats_k, dim3(nb, g.P), dim3(256), 0, s, th, g.P, Hl, Wl, f, c1, c2, part);
-    IC_CHECK_LAUNCH();
+    int nb;
+    if (fused_ok(g)) {
+      int tx, ty;
+      nb = fwd_tiles(g, l, tx, ty);
+      hipLaunchKernelGGL(ssim_fwd_tile_k<FMAX>, dim3(tx, ty, g.P), dim3(256), 0, s, al, bl, Hl, Wl, f, c1, c2, part);
+      IC_CHECK_LAUNCH();
+    } else {
+      const long long nhf = (long long)g.P * Hl * (Wl - g.fs + 1);
+      hipLaunchKernelGGL(hfilt_k, dim3(grid_for(nhf)), dim3(256), 0, s, al, bl, g.P, Hl, Wl, f, th);
+      IC_CHECK_LAUNCH();
+      nb = vstats_blocks(Hl - g.fs + 1, Wl - g.fs + 1);
+      hipLaunchKernelGGL(vstats_k, dim3(nb, g.P), dim3(256), 0, s, th, g.P, Hl, Wl, f, c1, c2, part);
+      IC_CHECK_LAUNCH();
+    }
     hipLaunchKernelGGL(vstats_final_k, dim3((g.P + 255) / 256), dim3(256), 0, s, part, g.P, nb,
                        state + g.stats_off + (long long)l * g.P * 2);
     IC_CHECK_LAUNCH();
@@ -449,10 +651,11 @@ int ic_msssim_bwd(int N, int C, int H, int W, int nlev, int filter_size, float f
   const Filt f = make_filt(filter_size, filter_sigma);
   const float c1 = (k1 * max_val) * (k1 * max_val), c2 = (k2 * max_val) * (k2 * max_val);
   const long long Wv0 = g.W[0] - g.fs + 1, Hv0 = g.H[0] - g.fs + 1;
+  const bool fz = fused_ok(g);
   char* p = (char*)ws;
-  float* th = (float*)p; p += ic_align((size_t)5 * g.P * g.H[0] * Wv0 * 4, 256);
-  float* D = (float*)p; p += ic_align((size_t)5 * g.P * Hv0 * Wv0 * 4, 256);
-  float* E = (float*)p; p += ic_align((size_t)5 * g.P * g.H[0] * Wv0 * 4, 256);
+  float* th = (float*)p; p += fz ? 0 : ic_align((size_t)5 * g.P * g.H[0] * Wv0 * 4, 256);
+  float* D = (float*)p; p += fz ? 0 : ic_align((size_t)5 * g.P * Hv0 * Wv0 * 4, 256);
+  float* E = (float*)p; p += fz ? 0 : ic_align((size_t)5 * g.P * g.H[0] * Wv0 * 4, 256);
   float* grads = (float*)p;
   long long goff[MAXLEV];
   long long gt = 0;
@@ -475,6 +678,12 @@ int ic_msssim_bwd(int N, int C, int H, int W, int nlev, int filter_size, float f
       hipLaunchKernelGGL(down_adj_k, dim3(grid_for(2 * nl)), dim3(256), 0, s, grads + goff[l + 1], 2 * g.P, Hl, Wl,
                          gal);
       IC_CHECK_LAUNCH();
+    }
+    if (fz) {
+      hipLaunchKernelGGL(ssim_bwd_tile_k<FMAX>, dim3((Wl + BTW - 1) / BTW, (Hl + BTH - 1) / BTH, g.P), dim3(256), 0, s, al,
+                         bl, g.C, Hl, Wl, f, c1, c2, coef + (long long)l * g.N * 2, gal, gbl);
+      IC_CHECK_LAUNCH();
+      continue;
     }
     const long long Wv = Wl - g.fs + 1, Hv = Hl - g.fs + 1;
     const long long nhf = (long long)g.P * Hl * Wv, nv = (long long)g.P * Hv * Wv;

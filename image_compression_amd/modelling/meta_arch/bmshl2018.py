@@ -4,6 +4,8 @@ modelling/meta_arch/bmshl2018.py:49-110), every tensor op on HIP kernels.
 forward(x) -> (x_tilde.detach(), losses) with losses =
 {z_entropy, y_entropy, bpp, total_loss, <distortion names>}; only
 total_loss carries grad."""
+import os
+
 import torch
 import torch.nn as nn
 
@@ -46,8 +48,10 @@ def side_stream(device):
     profiles/r05s_side_priority_ab.txt)."""
     k = device.index if device.index is not None else torch.cuda.current_device()
     if k not in _SIDE:
-        _SIDE[k] = torch.cuda.Stream(device=device, priority=0)
-        _WGRAD[k] = torch.cuda.Stream(device=device, priority=0)
+        # IMGCOMP_SIDE_PRIORITY: stream priority of the two (0 normal, -1 high); diagnostic A/B knob
+        prio = int(os.environ.get("IMGCOMP_SIDE_PRIORITY", "0"))
+        _SIDE[k] = torch.cuda.Stream(device=device, priority=prio)
+        _WGRAD[k] = torch.cuda.Stream(device=device, priority=prio)
         route_weight_gradients(_SIDE[k], _WGRAD[k])
     return _SIDE[k]
 
