@@ -44,6 +44,14 @@ def test_workspace_queries_without_gpu():
     assert L.ic_conv2d_fwd_ws(a, 5, 2, 2, bad) == 0
     assert L.ic_msssim_state_bytes(2, 3, 64, 64, 5, 11) == 0  # too small for 5 levels
     assert L.ic_msssim_state_bytes(2, 3, 192, 192, 5, 11) > 0
+    # the fused MS-SSIM forward writes one (cs, ssim) partial per 64 x 16 tile of valid outputs and plane:
+    # a Kodak-sized image (758 x 502 valid outputs at level 0 = 12 x 32 tiles) needs more than the
+    # round-4 fixed 64 partials per plane
+    assert L.ic_msssim_ws(1, 3, 512, 768, 5, 11) >= 3 * 12 * 32 * 2 * 4
+    # the fused backward needs no moment / derivative planes: C4's workspace is the per-level gradients
+    n0 = 16 * 3 * 256 * 256
+    grads = sum(2 * n0 // 4 ** l for l in range(5)) * 4
+    assert grads <= L.ic_msssim_ws(16, 3, 256, 256, 5, 11) < grads + 4 * 1024 * 1024
 
 
 def test_cpu_tensors_fail_loudly():

@@ -19,11 +19,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--math", type=int, default=2)
+    ap.add_argument("--sizes", default="128,64,32", help="map sizes (comma-separated)")
     a = ap.parse_args()
     L = _lib.load()
     st = _lib.c_void(torch.cuda.current_stream().cuda_stream)
     print("lib", os.environ.get("IMGCOMP_LIB", "in-tree"))
-    for h in (128, 64, 32):
+    for h in [int(v) for v in a.sizes.split(",")]:
         C, N = 192, 32
         g = torch.Generator(device="cuda").manual_seed(0)
         x = torch.randn(N, C, h, h, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)

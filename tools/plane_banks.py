@@ -18,7 +18,8 @@ def conflicts(addr_dwords_per_lane, groups, nbanks):
                 b=d%nbanks; cnt.setdefault(b,set()).add(d)
         worst=max(worst,max(len(v) for v in cnt.values()))
     return worst
-for name,sw in (('old',pl_sw_old),('new',pl_sw_new)):
+def simulate(sw):
+    """(worst n-way of the dx b128 fragment reads, of the tr reads, of the phase-A b64 stores)"""
     # (1) dx A/B fragment b128: lane (li,lg): row li, channels 32s+8lg..+7
     w1=1
     for s in range(6):
@@ -45,4 +46,10 @@ for name,sw in (('old',pl_sw_old),('new',pl_sw_new)):
                 li,lg=lane&15,lane>>4
                 e=off(li,48*w+4*lg+16*j,sw); A.append([e//2,e//2+1])
             w3=max(w3,conflicts(A,[list(range(16*g,16*g+16)) for g in range(4)],32))
-    print(name,'b128 dx frag',w1,'tr',w2,'phaseA b64 write',w3)
+    return w1,w2,w3
+
+
+if __name__ == "__main__":
+    for name,sw in (('old',pl_sw_old),('new',pl_sw_new)):
+        w1,w2,w3=simulate(sw)
+        print(name,'b128 dx frag',w1,'tr',w2,'phaseA b64 write',w3)
