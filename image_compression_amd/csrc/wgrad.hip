@@ -12,7 +12,6 @@
 // they sit in NHWC memory); a half-wave reads 32 consecutive floats of one row
 // per operand fragment (ds_read_b32, conflict-free).
 #include "gemm.h"
-#include <type_traits>
 #include <algorithm>
 
 #ifndef WG_X3_TWO
@@ -730,9 +729,6 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #ifndef WG_X3G_ABL
 #define WG_X3G_ABL 0  // diagnostic ablations of wg_x3g_kernel (wrong results): 1 no G staging, 2 no X staging, 4 no MFMAs
 #endif
-#ifndef WG_X3G_STAGGER
-#define WG_X3G_STAGGER 1  // wg_x3g_kernel: the two waves of a SIMD stage after alternate row tiles
-#endif
 #ifndef WG_X3_DUAL16
 #define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
 #endif
@@ -1100,11 +1096,7 @@ __device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int sp
     const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + xo_hi[j]));
     return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
-  // STAG: the row tile after which a wave stores and refills its staged slots -- waves 0-3 after the odd
-  // row tiles, waves 4-7 (the second wave of each SIMD) after the even ones (WG_X3G_STAGGER), so the two
-  // waves of a SIMD do not run their VALU / LDS-store phases at the same time
-  auto step = [&](auto stag_c, int p0, int buf, floatx4v (&rg)[QG], floatx4v (&rx)[QX]) {
-    constexpr int STAG = decltype(stag_c)::value;
+  auto step = [&](int p0, int buf, floatx4v (&rg)[QG], floatx4v (&rx)[QX]) {
     const __bf16* sb = lds + buf * STAGE;
     b8 bb[NP][TN];
 #pragma unroll
@@ -1132,7 +1124,7 @@ __device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int sp
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
         }
       }
-      if ((i & 1) != STAG) {
+      if (i & 1) {
         // the next step's split + store of slot i / 2, then its refill three steps ahead
         sstore_q(buf ^ 1, i >> 1, rg, rx);
         gload_q(nb, i >> 1, rg, rx);
@@ -1157,16 +1149,9 @@ __device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int sp
     gload(q0 + 2 * BK, gr0, xr0, q0 + 2 * BK < pe);
   }
   __syncthreads();
-  if (WG_X3G_STAGGER && wm) {
-    for (int p0 = q0; p0 < pe; p0 += 2 * BK) {
-      step(std::integral_constant<int, 1>{}, p0, 0, gr1, xr1);
-      step(std::integral_constant<int, 1>{}, p0 + BK, 1, gr0, xr0);
-    }
-  } else {
-    for (int p0 = q0; p0 < pe; p0 += 2 * BK) {
-      step(std::integral_constant<int, 0>{}, p0, 0, gr1, xr1);
-      step(std::integral_constant<int, 0>{}, p0 + BK, 1, gr0, xr0);
-    }
+  for (int p0 = q0; p0 < pe; p0 += 2 * BK) {
+    step(p0, 0, gr1, xr1);
+    step(p0 + BK, 1, gr0, xr0);
   }
 
   // C/D map of the 16x16 MFMA: row (g) = 4 lq + r, col = li; column tile j belongs to tap tt
