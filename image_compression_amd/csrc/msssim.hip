@@ -351,9 +351,46 @@ __global__ void scale_out_k(const float* ga, const float* gb, long long n, float
 constexpr int FMAX = 11;                      // fused kernels: filter size 11 (every reference config)
 constexpr int FTW = 64, FTH = 16;             // forward: valid outputs per tile
 constexpr int FRW = FTW + FMAX - 1, FRH = FTH + FMAX - 1;
+constexpr int FAP = 76;                       // forward input pitch (>= FRW, four-aligned 14-wide windows)
 constexpr int BTW = 32, BTH = 16;             // backward: gradient pixels per tile
 constexpr int BDW = BTW + FMAX - 1, BDH = BTH + FMAX - 1;          // derivative-map region
+constexpr int BDP = 44;                       // its pitch: 11 groups of four columns
 constexpr int BIW = BTW + 2 * (FMAX - 1), BIH = BTH + 2 * (FMAX - 1);  // input region
+constexpr int BAP = 56;                       // backward input pitch (>= BDP + 12)
+static_assert(FRW <= FAP && FAP >= FTW + 12 && BDW <= BDP && BIW <= BAP && BAP >= BDP + 12, "tile pitches");
+
+// Every pass of the fused kernels works on four consecutive columns per thread: the 14 inputs a
+// four-output window of the 11-tap filter needs are four 16-B LDS reads (three to five times fewer LDS
+// instructions than one column per thread, which left the level-0 backward LDS-bound), and the
+// division-heavy SSIM formulas use one reciprocal per denominator (v_rcp_f32, 1 ulp: relative ~1e-7,
+// far inside the 1e-4 bar).
+__device__ __forceinline__ void ld16(const float* p, float (&v)[16]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const floatx4v t = *(const floatx4v*)(p + 4 * k);
+    v[4 * k] = t[0]; v[4 * k + 1] = t[1]; v[4 * k + 2] = t[2]; v[4 * k + 3] = t[3];
+  }
+}
+__device__ __forceinline__ void st4(float* p, const float (&v)[4]) { *(floatx4v*)p = floatx4v{v[0], v[1], v[2], v[3]}; }
+__device__ __forceinline__ floatx4v ld4(const float* p) { return *(const floatx4v*)p; }
+
+// horizontal pass of one row, four output columns: m[q][o] = sum_k g[k] mom_q(a[o + k], b[o + k])
+template <int FS>
+__device__ __forceinline__ void hmom4(const float* ar, const float* br, const Filt& f, float (&m)[5][4]) {
+  float va[16], vb[16];
+  ld16(ar, va);
+  ld16(br, vb);
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+#pragma unroll
+    for (int k = 0; k < FS; ++k) {
+      const float g = f.g[k], x = va[o + k], y = vb[o + k];
+      s0 += g * x; s1 += g * y; s2 += g * (x * x); s3 += g * (y * y); s4 += g * (x * y);
+    }
+    m[0][o] = s0; m[1][o] = s1; m[2][o] = s2; m[3][o] = s3; m[4][o] = s4;
+  }
+}
 
 // forward: per tile of FTW x FTH valid outputs, the per-plane partial sums of the cs and ssim maps
 // (part[p][tile][2], summed per plane in a fixed order by vstats_final_k)
@@ -362,11 +399,11 @@ template <int FS>
 __global__ void __launch_bounds__(256) ssim_fwd_tile_k(const float* __restrict__ a, const float* __restrict__ b,
                                                        int H, int W, const Filt f, float c1, float c2,
                                                        float* __restrict__ part) {
-  __shared__ float A[FRH][FRW], B[FRH][FRW];
-  __shared__ float HM[5][FRH][FTW];
+  static_assert(FS <= FMAX, "LDS regions sized for FMAX");
+  __shared__ __attribute__((aligned(16))) float A[FRH][FAP], B[FRH][FAP];
+  __shared__ __attribute__((aligned(16))) float HM[5][FRH][FTW];
   __shared__ float red[32];
   constexpr int fs = FS;
-  static_assert(FS <= FMAX, "LDS regions sized for FMAX");
   const int Wv = W - fs + 1, Hv = H - fs + 1;
   const int p = blockIdx.z;
   const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
@@ -374,40 +411,44 @@ __global__ void __launch_bounds__(256) ssim_fwd_tile_k(const float* __restrict__
   const float* pa = a + (long long)p * H * W;
   const float* pb = b + (long long)p * H * W;
   const int rw = min(FTW, Wv - x0) + fs - 1, rh = min(FTH, Hv - y0) + fs - 1;
-  for (int i = tid; i < FRH * FRW; i += 256) {
-    const int r = i / FRW, c = i - (i / FRW) * FRW;
+  for (int i = tid; i < FRH * FAP; i += 256) {
+    const int r = i / FAP, c = i - (i / FAP) * FAP;
     const bool in = r < rh && c < rw;
     const long long o = (long long)(y0 + r) * W + x0 + c;
     A[r][c] = in ? pa[o] : 0.f;
     B[r][c] = in ? pb[o] : 0.f;
   }
   __syncthreads();
-  // horizontal pass: HM[q][r][c] = sum_k g[k] m_q(r, c + k)
-  for (int i = tid; i < FRH * FTW; i += 256) {
-    const int r = i / FTW, c = i - (i / FTW) * FTW;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
-    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
-      const float g = f.g[k], va = A[r][c + k], vb = B[r][c + k];
-      s0 += g * va; s1 += g * vb; s2 += g * (va * va); s3 += g * (vb * vb); s4 += g * (va * vb);
-    }
-    HM[0][r][c] = s0; HM[1][r][c] = s1; HM[2][r][c] = s2; HM[3][r][c] = s3; HM[4][r][c] = s4;
+  for (int i = tid; i < FRH * (FTW / 4); i += 256) {
+    const int r = i / (FTW / 4), c = 4 * (i - (i / (FTW / 4)) * (FTW / 4));
+    float m[5][4];
+    hmom4<FS>(&A[r][c], &B[r][c], f, m);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) st4(&HM[q][r][c], m[q]);
   }
   __syncthreads();
   float v0 = 0.f, v1 = 0.f;
-  for (int i = tid; i < FTH * FTW; i += 256) {
-    const int r = i / FTW, c = i - (i / FTW) * FTW;
-    if (y0 + r >= Hv || x0 + c >= Wv) continue;
-    float ma = 0.f, mb = 0.f, saa = 0.f, sbb = 0.f, sab = 0.f;
-    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+  for (int i = tid; i < FTH * (FTW / 4); i += 256) {
+    const int r = i / (FTW / 4), c = 4 * (i - (i / (FTW / 4)) * (FTW / 4));
+    floatx4v mm[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) mm[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < FS; ++k) {
       const float g = f.g[k];
-      ma += g * HM[0][r + k][c]; mb += g * HM[1][r + k][c]; saa += g * HM[2][r + k][c];
-      sbb += g * HM[3][r + k][c]; sab += g * HM[4][r + k][c];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) mm[q] += g * ld4(&HM[q][r + k][c]);
     }
-    const float mu12 = ma * mb;
-    const float s1 = saa - ma * ma, s2 = sbb - mb * mb, s12 = sab - mu12;
-    const float cs = (2.f * s12 + c2) / (s1 + s2 + c2);
-    v0 += cs;
-    v1 += cs * (2.f * mu12 + c1) / (ma * ma + mb * mb + c1);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (y0 + r >= Hv || x0 + c + o >= Wv) continue;
+      const float ma = mm[0][o], mb = mm[1][o];
+      const float mu12 = ma * mb;
+      const float s1 = mm[2][o] - ma * ma, s2 = mm[3][o] - mb * mb, s12 = mm[4][o] - mu12;
+      const float cs = (2.f * s12 + c2) * __builtin_amdgcn_rcpf(s1 + s2 + c2);
+      v0 += cs;
+      v1 += cs * (2.f * mu12 + c1) * __builtin_amdgcn_rcpf(ma * ma + mb * mb + c1);
+    }
   }
   float v[2] = {v0, v1};
   block_sum<2>(v, red);
@@ -420,100 +461,121 @@ __global__ void __launch_bounds__(256) ssim_fwd_tile_k(const float* __restrict__
 
 // backward: per tile of BTW x BTH pixels of a level, the gradient contribution of that level's map
 // sums (coef_l = dLoss / d(per-pixel cs, ssim) for each image), accumulated into (ga, gb).
-//   D (five maps) at the valid outputs whose windows reach the tile, from the moments recomputed
-//   there; E = vertical adjoint of D on the tile rows; the horizontal adjoint and the moments' chain
-//   rule onto the tile pixels (as dmaps_k -> vadj_k -> hadj_k)
+//   D (four maps: d/d ma, mb, saa = sbb, sab) at the valid outputs whose windows reach the tile, from
+//   the moments recomputed there; E = vertical adjoint of D on the tile rows; the horizontal adjoint
+//   and the moments' chain rule onto the tile pixels (as dmaps_k -> vadj_k -> hadj_k)
 template <int FS>
 __global__ void __launch_bounds__(256) ssim_bwd_tile_k(const float* __restrict__ a, const float* __restrict__ b,
                                                        int C, int H, int W, const Filt f, float c1, float c2,
                                                        const float* __restrict__ coef_l, float* __restrict__ ga,
                                                        float* __restrict__ gb) {
-  __shared__ float A[BIH][BIW], B[BIH][BIW];
-  __shared__ float HM[5][BIH][BDW];  // horizontal moments; then E[5][BTH][BDW] in its first rows
-  __shared__ float D[4][BDH][BDW];   // d/d(ma, mb, saa = sbb, sab)
-  constexpr int fs = FS, h = FS - 1;
   static_assert(FS <= FMAX, "LDS regions sized for FMAX");
+  __shared__ __attribute__((aligned(16))) float A[BIH][BAP], B[BIH][BAP];
+  __shared__ __attribute__((aligned(16))) float HM[5][BIH][BDP];  // horizontal moments; then E[4][BTH][BDP]
+  __shared__ __attribute__((aligned(16))) float D[4][BDH][BDP];
+  constexpr int fs = FS, h = FS - 1;
+  constexpr int NC = BDP / 4;  // column groups of the moment / derivative regions
   const int Wv = W - fs + 1, Hv = H - fs + 1;
   const int p = blockIdx.z, n = p / C;
   const int x0 = blockIdx.x * BTW, y0 = blockIdx.y * BTH;
   const int ox = x0 - h, oy = y0 - h;  // origin of the input and D regions
-  constexpr int iw = BTW + 2 * h, ih = BTH + 2 * h, dw = BTW + h, dh = BTH + h;
+  constexpr int ih = BTH + 2 * h, dh = BTH + h, dw = BTW + h;
   const int tid = threadIdx.x;
   const float* pa = a + (long long)p * H * W;
   const float* pb = b + (long long)p * H * W;
   const float gC = coef_l[n * 2], gS = coef_l[n * 2 + 1];
-  for (int i = tid; i < ih * iw; i += 256) {
-    const int r = i / iw, c = i - (i / iw) * iw;
+  for (int i = tid; i < ih * BAP; i += 256) {
+    const int r = i / BAP, c = i - (i / BAP) * BAP;
     const int y = oy + r, x = ox + c;
-    const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && c < BIW;
     const long long o = (long long)y * W + x;
     A[r][c] = in ? pa[o] : 0.f;
     B[r][c] = in ? pb[o] : 0.f;
   }
   __syncthreads();
-  for (int i = tid; i < ih * dw; i += 256) {
-    const int r = i / dw, c = i - (i / dw) * dw;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
-    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
-      const float g = f.g[k], va = A[r][c + k], vb = B[r][c + k];
-      s0 += g * va; s1 += g * vb; s2 += g * (va * va); s3 += g * (vb * vb); s4 += g * (va * vb);
-    }
-    HM[0][r][c] = s0; HM[1][r][c] = s1; HM[2][r][c] = s2; HM[3][r][c] = s3; HM[4][r][c] = s4;
+  for (int i = tid; i < ih * NC; i += 256) {
+    const int r = i / NC, c = 4 * (i - (i / NC) * NC);
+    float m[5][4];
+    hmom4<FS>(&A[r][c], &B[r][c], f, m);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) st4(&HM[q][r][c], m[q]);
   }
   __syncthreads();
-  for (int i = tid; i < dh * dw; i += 256) {
-    const int r = i / dw, c = i - (i / dw) * dw;
-    const int yv = oy + r, xv = ox + c;
-    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d4 = 0.f;
-    if ((unsigned)yv < (unsigned)Hv && (unsigned)xv < (unsigned)Wv) {
-      float ma = 0.f, mb = 0.f, saa = 0.f, sbb = 0.f, sab = 0.f;
-      _Pragma("unroll") for (int k = 0; k < fs; ++k) {
-        const float g = f.g[k];
-        ma += g * HM[0][r + k][c]; mb += g * HM[1][r + k][c]; saa += g * HM[2][r + k][c];
-        sbb += g * HM[3][r + k][c]; sab += g * HM[4][r + k][c];
-      }
-      const float A1 = 2.f * ma * mb + c1, B1 = ma * ma + mb * mb + c1;
-      const float A2 = 2.f * (sab - ma * mb) + c2;
-      const float B2 = (saa - ma * ma) + (sbb - mb * mb) + c2;
-      const float cs = A2 / B2, lum = A1 / B1;
-      const float ucs = gC + gS * lum, ul = gS * cs;
-      const float gA2 = ucs / B2, gB2 = -ucs * A2 / (B2 * B2);
-      const float gA1 = ul / B1, gB1 = -ul * A1 / (B1 * B1);
-      d0 = -2.f * mb * gA2 - 2.f * ma * gB2 + 2.f * mb * gA1 + 2.f * ma * gB1;
-      d1 = -2.f * ma * gA2 - 2.f * mb * gB2 + 2.f * ma * gA1 + 2.f * mb * gB1;
-      d2 = gB2;
-      d4 = 2.f * gA2;
+  for (int i = tid; i < dh * NC; i += 256) {
+    const int r = i / NC, c = 4 * (i - (i / NC) * NC);
+    floatx4v mm[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) mm[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < FS; ++k) {
+      const float g = f.g[k];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) mm[q] += g * ld4(&HM[q][r + k][c]);
     }
-    D[0][r][c] = d0; D[1][r][c] = d1; D[2][r][c] = d2; D[3][r][c] = d4;
+    float d[4][4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int yv = oy + r, xv = ox + c + o;
+      const bool valid = (unsigned)yv < (unsigned)Hv && (unsigned)xv < (unsigned)Wv && c + o < dw;
+      const float ma = mm[0][o], mb = mm[1][o];
+      const float A1 = 2.f * ma * mb + c1, B1 = ma * ma + mb * mb + c1;
+      const float A2 = 2.f * (mm[4][o] - ma * mb) + c2;
+      const float B2 = (mm[2][o] - ma * ma) + (mm[3][o] - mb * mb) + c2;
+      const float iB1 = __builtin_amdgcn_rcpf(B1), iB2 = __builtin_amdgcn_rcpf(B2);
+      const float cs = A2 * iB2, lum = A1 * iB1;
+      const float ucs = gC + gS * lum, ul = gS * cs;
+      const float gA2 = ucs * iB2, gB2 = -gA2 * cs;   // -ucs A2 / B2^2
+      const float gA1 = ul * iB1, gB1 = -gA1 * lum;   // -ul A1 / B1^2
+      d[0][o] = valid ? -2.f * mb * gA2 - 2.f * ma * gB2 + 2.f * mb * gA1 + 2.f * ma * gB1 : 0.f;
+      d[1][o] = valid ? -2.f * ma * gA2 - 2.f * mb * gB2 + 2.f * ma * gA1 + 2.f * mb * gB1 : 0.f;
+      d[2][o] = valid ? gB2 : 0.f;
+      d[3][o] = valid ? 2.f * gA2 : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st4(&D[q][r][c], d[q]);
   }
   __syncthreads();
   // vertical adjoint onto the tile rows: E[q][y][c] = sum_k g[k] D[q][y + h - k][c]  (E over HM)
-  float (*E)[BIH][BDW] = HM;
-  for (int i = tid; i < BTH * dw; i += 256) {
-    const int y = i / dw, c = i - (i / dw) * dw;
-    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e4 = 0.f;
-    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
+  float (*E)[BIH][BDP] = HM;
+  for (int i = tid; i < BTH * NC; i += 256) {
+    const int y = i / NC, c = 4 * (i - (i / NC) * NC);
+    floatx4v e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < FS; ++k) {
       const float g = f.g[k];
-      const int r = y + h - k;
-      e0 += g * D[0][r][c]; e1 += g * D[1][r][c]; e2 += g * D[2][r][c]; e4 += g * D[3][r][c];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[q] += g * ld4(&D[q][y + h - k][c]);
     }
-    E[0][y][c] = e0; E[1][y][c] = e1; E[2][y][c] = e2; E[3][y][c] = e4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(floatx4v*)&E[q][y][c] = e[q];
   }
   __syncthreads();
   // horizontal adjoint and the moments' chain rule (hadj_k): s_q[y][x] = sum_k g[k] E[q][y][x + h - k]
-  for (int i = tid; i < BTH * BTW; i += 256) {
-    const int y = i / BTW, x = i - (i / BTW) * BTW;
-    if (y0 + y >= H || x0 + x >= W) continue;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s4 = 0.f;
-    _Pragma("unroll") for (int k = 0; k < fs; ++k) {
-      const float g = f.g[k];
-      const int c = x + h - k;
-      s0 += g * E[0][y][c]; s1 += g * E[1][y][c]; s2 += g * E[2][y][c]; s4 += g * E[3][y][c];
+  for (int i = tid; i < BTH * (BTW / 4); i += 256) {
+    const int y = i / (BTW / 4), x = 4 * (i - (i / (BTW / 4)) * (BTW / 4));
+    float s[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float ev[16];
+      ld16(&E[q][y][x], ev);  // columns x .. x + 15 hold x + h - k for k = 0..10 and the four outputs
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < FS; ++k) t += f.g[k] * ev[o + h - k];
+        s[q][o] = t;
+      }
     }
-    const float va = A[y + h][x + h], vb = B[y + h][x + h];
-    const long long o = (long long)p * H * W + (long long)(y0 + y) * W + x0 + x;
-    ga[o] += s0 + 2.f * va * s2 + vb * s4;
-    gb[o] += s1 + 2.f * vb * s2 + va * s4;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (y0 + y >= H || x0 + x + o >= W) continue;
+      const float va = A[y + h][x + o + h], vb = B[y + h][x + o + h];
+      const long long off = (long long)p * H * W + (long long)(y0 + y) * W + x0 + x + o;
+      ga[off] += s[0][o] + 2.f * va * s[2][o] + vb * s[3][o];
+      gb[off] += s[1][o] + 2.f * vb * s[2][o] + va * s[3][o];
+    }
   }
 }
 

@@ -84,6 +84,79 @@ __global__ void pack_fast_kernel(const PackArgs p) {
     store_packed(p, (long long)((uint32_t)t * nr + i), (long long)total, v);
   }
 }
+
+// tiled fast layouts (mode 0 / 1, k <= 5, R even, B % 4 == 0): one block per PK_TN x PK_TR tile of
+// (n, r), all taps.  The tile's source is PK_TN (mode 0) or PK_TR (mode 1) runs of contiguous floats
+// (a row of W[a][b][ky][kx] over (b, tap) or over (a-fixed) (n, tap)): staged through LDS with 16-B
+// loads, about three per thread and all in flight together, then written with four tap groups of 64
+// threads, two consecutive r per thread (one 4-B store per plane).  The per-element kernel
+// (pack_fast_kernel) reads W with a stride of k*k floats (mode 0) or B*k*k floats (mode 1) per lane,
+// a cache line per lane: 30-40 us per 192 x 192 5x5 weight on the main queue, 12 per C2 step.
+typedef __bf16 pk_bf16x2 __attribute__((ext_vector_type(2)));
+constexpr int PK_TN = 4, PK_TR = 32, PK_NT = 256;
+__global__ void __launch_bounds__(PK_NT) pack_tile_kernel(const PackArgs p) {
+  __shared__ __attribute__((aligned(16))) float ws[PK_TN * PK_TR * 25];
+  const int Nout = p.mode == 0 ? p.A : p.B;
+  const int R = p.mode == 0 ? p.B : p.A;
+  const int kk = p.k * p.k;
+  const int r0 = blockIdx.x * PK_TR, n0 = blockIdx.y * PK_TN;
+  const int tid = threadIdx.x;
+  // rows of the tile's source: mode 0 rows n (PK_TR * kk floats each), mode 1 rows r (PK_TN * kk)
+  const int nrows = p.mode == 0 ? PK_TN : PK_TR;
+  const int len = (p.mode == 0 ? PK_TR : PK_TN) * kk;  // a multiple of 4
+  const int row0 = p.mode == 0 ? n0 : r0, rowmax = p.mode == 0 ? Nout : R;
+  const int valid = p.mode == 0 ? min(PK_TR, R - r0) * kk : max(0, min(PK_TN, Nout - n0)) * kk;
+  const int col0 = p.mode == 0 ? r0 : n0;
+  const int nv = nrows * (len >> 2);
+#pragma unroll 4
+  for (int j = tid; j < nv; j += PK_NT) {
+    const int row = j / (len >> 2), q = 4 * (j - row * (len >> 2));
+    const int gr = row0 + row;
+    const float* src = p.W + ((long long)gr * p.B + col0) * kk + q;
+    float v[4];
+    if (gr < rowmax && q + 3 < valid) {
+      const float4 t = *(const float4*)src;
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (gr < rowmax && q + e < valid) ? src[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int qq = q + e;
+      if (p.mode == 0) {
+        ws[row * len + qq] = v[e];  // [nl][rl][tap]
+      } else {
+        const int nl = qq / kk, tap = qq - nl * kk;
+        ws[(nl * PK_TR + row) * kk + tap] = v[e];
+      }
+    }
+  }
+  __syncthreads();
+  const long long nrow = (long long)p.Npad * R, total = (long long)p.T * nrow;
+  const int tg = tid >> 6, l = tid & 63;
+  const int nl = l >> 4, rl = 2 * (l & 15);
+  const int n = n0 + nl, r = r0 + rl;
+  if (n >= p.Npad || r >= R) return;
+  for (int t = tg; t < p.T; t += PK_NT / 64) {
+    const int toff = p.ky[t] * p.k + p.kx[t];
+    const float v0 = ws[(nl * PK_TR + rl) * kk + toff], v1 = ws[(nl * PK_TR + rl + 1) * kk + toff];
+    const long long i = t * nrow + (long long)n * R + r;
+    if (p.out_bf16 == 2) {
+      __bf16 h0, m0, l0, h1, m1, l1;
+      split3_bf16(v0, h0, m0, l0);
+      split3_bf16(v1, h1, m1, l1);
+      __bf16* o = (__bf16*)p.wp;
+      *(pk_bf16x2*)(o + i) = pk_bf16x2{h0, h1};
+      *(pk_bf16x2*)(o + i + total) = pk_bf16x2{m0, m1};
+      *(pk_bf16x2*)(o + i + 2 * total) = pk_bf16x2{l0, l1};
+    } else if (p.out_bf16) {
+      *(pk_bf16x2*)((__bf16*)p.wp + i) = pk_bf16x2{(__bf16)v0, (__bf16)v1};
+    } else {
+      *(float2*)(p.wp + i) = make_float2(v0, v1);
+    }
+  }
+}
 }  // namespace
 
 int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int T, const int* ky,
@@ -95,6 +168,11 @@ int pack_weights(const float* W, int A, int B, int k, int mode, int generic, int
   for (int t = 0; t < T; ++t) { p.ky[t] = ky[t]; p.kx[t] = kx[t]; }
   const int R = mode == 0 ? B : A;
   const long long total = mode == 2 ? (long long)Npad * A : (generic ? (long long)Npad * Kpad : (long long)T * Npad * R);
+  if (!generic && mode < 2 && k <= 5 && R % 2 == 0 && B % 4 == 0 && ((uintptr_t)W & 15) == 0 && total < (1ll << 31)) {
+    hipLaunchKernelGGL(pack_tile_kernel, dim3((R + PK_TR - 1) / PK_TR, (Npad + PK_TN - 1) / PK_TN), dim3(PK_NT), 0, s, p);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   if (!generic && mode < 2 && total < (1ll << 31)) {
     const long long nr = (long long)Npad * R;
     long long blocks = (nr + 255) / 256;

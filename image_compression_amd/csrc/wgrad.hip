@@ -729,6 +729,16 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #ifndef WG_X3G_ABL
 #define WG_X3G_ABL 0  // diagnostic ablations of wg_x3g_kernel (wrong results): 1 no G staging, 2 no X staging, 4 no MFMAs
 #endif
+#ifndef WG_X3P
+#define WG_X3P 1  // the tap-group weight gradients on producer / consumer waves (wg_x3p_kernel); 0: wg_x3g_kernel
+#endif
+#ifndef WG_X3P_PRIO
+#define WG_X3P_PRIO 0  // s_setprio of the producer waves (0: hardware default)
+#endif
+#ifndef WG_X3P_ABL
+#define WG_X3P_ABL 0  // diagnostic ablations of wg_x3p_kernel (wrong results): 1 no global loads, 2 no LDS stores, 4 no MFMAs, 8 every step loads the split's first pixels (L2-hot), 16 no split (one
+// conversion per value), 32 every step loads step 0 (loop-invariant addresses)
+#endif
 #ifndef WG_X3_DUAL16
 #define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
 #endif
@@ -1175,6 +1185,249 @@ __device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int sp
     for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
 }
 
+// Producer / consumer tap groups (WG_X3P, round 5): wg_x3g_body's tiles, LDS images, MFMAs and their
+// order (so bitwise its result), with the staging moved off the MFMA waves.  Twelve waves, three per
+// SIMD: the eight consumer waves only read fragments and run the MFMAs of step s from one LDS stage;
+// the four producer waves (one per SIMD) meanwhile split and store step s + 1 into the other stage
+// and load step s + 3 into the register set it frees (two sets, loads two steps ahead).  One barrier
+// per step for all twelve.  In wg_x3g the split + store of the next step sat in each MFMA wave's
+// instruction stream (0.36 ms of a 1.19 ms g_a.2 wgrad: WG_X3G_ABL, profiles/r06k_*); a producer wave
+// issues its VALU and LDS stores while its SIMD's MFMA pipe is busy with the consumers' work.
+template <bool XSQ, int NTAP, int NP>
+__device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int split, int ky, int ct) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  constexpr int CW = 192 / NTAP;          // X channels per block
+  constexpr int BM = 192, WM = 96, WN = 48, BK = 32;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int PITCH = 192;
+  constexpr int XR = BK + NTAP - 1;       // X pixel rows per step
+  constexpr int GPLANE = BK * PITCH, XPLANE = 34 * PITCH;
+  constexpr int GOPER = NP * GPLANE;
+  constexpr int STAGE = NP * (GPLANE + XPLANE);
+  constexpr int NC = 512, NPR = 256;      // consumer / producer threads
+  constexpr int QG = BK * (BM / 4) / NPR; // 6 float4 of G per producer thread and step
+  constexpr int XQ4 = XR * (CW / 4);      // float4 of X per step
+  constexpr int QX = (XQ4 + NPR - 1) / NPR;  // 3 (NTAP 3) or 4 (NTAP 2)
+  static_assert(QG * NPR == BK * BM / 4, "G slots");
+  const int kx0 = NTAP == 3 ? 0 : 1;
+  const int t0 = ky * 5 + kx0;
+  const int c0 = ct * CW;
+  const int pb = split * d.pps;
+  int pe = pb + d.pps;
+  if (pe > (int)d.P) pe = (int)d.P;
+  const int nsteps = pe > pb ? (pe - pb) / BK : 0;
+  const int q0 = pb - ((nsteps & 1) ? BK : 0);  // an odd count starts with one all-zero (dead) step
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto swz = [](int row) { return ((((row >> 1) & 1) << 5) | (((row >> 3) & 1) << 4)); };
+
+  if (w >= NC / 64) {
+    // ---------------------------------------------------------------- producer waves
+    // WG_X3P_PRIO: the producers' issue priority over the consumer waves of their SIMD (the younger
+    // waves otherwise get only the VALU slots the older ones leave, and the barrier waits for them)
+    if (WG_X3P_PRIO) __builtin_amdgcn_s_setprio(WG_X3P_PRIO);
+    const int pt = tid - NC;
+    const int dyt = d.dy[t0], dx0 = d.dx[t0];
+    int grow[QG], gcol[QG], xrow[QX], xcol[QX];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+      const int f = pt + NPR * q;
+      grow[q] = f / (BM / 4);
+      gcol[q] = (f - grow[q] * (BM / 4)) * 4;
+    }
+#pragma unroll
+    for (int q = 0; q < QX; ++q) {
+      const int f = min(pt + NPR * q, XQ4 - 1);  // past the image: a second copy of the last float4
+      xrow[q] = f / (CW / 4);
+      xcol[q] = (f - xrow[q] * (CW / 4)) * 4;
+    }
+    uint32_t goff[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) goff[q] = ((uint32_t)grow[q] * (uint32_t)d.gs_w + (uint32_t)gcol[q]) * 4u;
+    floatx4v ga[QG] = {}, xa[QX] = {}, gb[QG] = {}, xb[QX] = {};
+    uint32_t oka = 0, okb = 0;
+    // step k of the block (pixels q0 + k BK ..).  Branch-free: every load reads an in-range address
+    // (dead steps pixel 0, padding a clamped column / row) and a select zeroes what must be zero; with
+    // a zero-page pointer select the compiler branched around each load on the uniform step flag and
+    // drained the loads in flight (s_waitcnt vmcnt(0)) inside the branches.
+    // the zeroing select is applied at the store (store()), so no value is consumed before its step
+    auto load = [&](int k, floatx4v (&rg)[QG], floatx4v (&rx)[QX], uint32_t& okm) {
+      if (WG_X3P_ABL & 32) k = 0;  // the first step's addresses every step (hoisted address math, L2-hot)
+      const int p0 = q0 + k * BK;
+      const bool live = p0 >= pb && p0 < pe;
+      const uint32_t pp = (WG_X3P_ABL & 8) ? (uint32_t)pb : live ? (uint32_t)p0 : 0u;
+      const uint32_t img = fdiv(pp, d.fd_hw);
+      const uint32_t rr = pp - img * d.fd_hw.d;
+      const uint32_t gy = fdiv(rr, d.fd_w);
+      const uint32_t gx0 = rr - gy * d.fd_w.d;
+      const int iy = (int)gy * 2 + dyt;
+      const bool rowok = live && (unsigned)iy < (unsigned)d.Hx;
+      const int iyc = min(max(iy, 0), d.Hx - 1);
+      // wave-uniform bases (SGPRs) + 32-bit per-lane byte offsets: the saddr form of global_load
+      const char* gbase = (const char*)(d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w);
+      const char* xbase = (const char*)(d.x + (long long)img * d.xs_n + (long long)iyc * d.xs_h + c0);
+#pragma unroll
+      for (int q = 0; q < QG; ++q)
+        if (!(WG_X3P_ABL & 1)) rg[q] = *(const floatx4v*)(gbase + goff[q]);
+      okm = live ? 1u : 0u;
+#pragma unroll
+      for (int q = 0; q < QX; ++q) {
+        const int ix = ((int)gx0 + xrow[q]) * 2 + dx0;
+        const bool ok = rowok && (unsigned)ix < (unsigned)d.Wx;
+        const uint32_t ixc = (uint32_t)min(max(ix, 0), d.Wx - 1);
+        if (!(WG_X3P_ABL & 1)) rx[q] = *(const floatx4v*)(xbase + (ixc * (uint32_t)d.xs_w + (uint32_t)xcol[q]) * 4u);
+        okm |= ok ? 2u << q : 0u;
+      }
+    };
+    auto put = [&](__bf16* dst, int plane, floatx4v v) {
+      if constexpr (NP == 1 || (WG_X3P_ABL & 16)) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        *(b4*)dst = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
+      } else {
+        b4 vh, vm, vl;
+        split3_bf16x4(v, vh, vm, vl);
+        *(b4*)dst = vh;
+        *(b4*)(dst + plane) = vm;
+        *(b4*)(dst + 2 * plane) = vl;
+      }
+    };
+    const floatx4v zero4 = {0.f, 0.f, 0.f, 0.f};
+    auto store = [&](int buf, const floatx4v (&rg)[QG], const floatx4v (&rx)[QX], uint32_t okm) {
+      if (WG_X3P_ABL & 2) return;
+      __bf16* base = lds + buf * STAGE;
+#pragma unroll
+      for (int q = 0; q < QG; ++q) {
+        put(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q])), GPLANE, (okm & 1u) ? rg[q] : zero4);
+        __builtin_amdgcn_sched_barrier(0);  // one slot at a time: the split temporaries of ten slots spilled
+      }
+#pragma unroll
+      for (int q = 0; q < QX; ++q) {
+        floatx4v v = (okm & (2u << q)) ? rx[q] : zero4;
+        if (XSQ) v = v * v;
+        put(base + GOPER + xrow[q] * PITCH + (xcol[q] ^ swz(xrow[q])), XPLANE, v);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    const int L = (pe - q0) / BK;  // steps run (even)
+    if (L > 0) {
+      load(0, ga, xa, oka);
+      load(1, gb, xb, okb);
+      store(0, ga, xa, oka);
+      load(2, ga, xa, oka);
+    }
+    __syncthreads();
+    for (int k = 0; k < L; k += 2) {
+      store(1, gb, xb, okb);  // step k + 1, while the consumers run step k
+      load(k + 3, gb, xb, okb);
+      __syncthreads();
+      store(0, ga, xa, oka);  // step k + 2, while the consumers run step k + 1
+      load(k + 4, ga, xa, oka);
+      __syncthreads();
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ consumer waves
+  const int wm = w >> 2, wn = w & 3;
+  const int li = lane & 15, lq = lane >> 4;
+  const int tr_r = 8 * lq + (li >> 2);
+  const int tr_c = 4 * (li & 3);
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  const int tr_sw = swz(tr_r);
+  auto tr8a = [&](const __bf16* plane, int col) {
+    const __bf16* src = plane + tr_r * PITCH + ((col + tr_c) ^ tr_sw);
+    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)src);
+    const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * PITCH));
+    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  int xo_lo[TN], xo_hi[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int vcol = wn * WN + 16 * j;
+    const int tt = vcol / CW, cc = vcol - (vcol / CW) * CW;
+    const int r0 = tr_r + tt;
+    xo_lo[j] = r0 * PITCH + ((cc + tr_c) ^ swz(r0));
+    xo_hi[j] = (r0 + 4) * PITCH + ((cc + tr_c) ^ swz(r0 + 4));
+  }
+  auto tr8b = [&](const __bf16* plane, int j) {
+    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + xo_lo[j]));
+    const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + xo_hi[j]));
+    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto step = [&](int buf) {
+    const __bf16* sb = lds + buf * STAGE;
+    b8 bb[NP][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) bb[q][j] = tr8b(sb + GOPER + q * XPLANE, j);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      b8 a[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[q] = tr8a(sb + q * GPLANE, wm * WM + 16 * i);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        floatx4v& c = acc[i][j];
+        if constexpr (NP == 1) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
+        } else if (!(WG_X3P_ABL & 4)) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bb[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[1][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[2][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[1][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  const int L = (pe - q0) / BK;
+  __syncthreads();
+  for (int k = 0; k < L; k += 2) {
+    step(0);
+    step(1);
+  }
+  // C/D map of the 16x16 MFMA: row (g) = 4 lq + r, col = li; column tile j belongs to tap tt
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int vcol = wn * WN + 16 * j;
+    const int tt = vcol / CW, cc = vcol - (vcol / CW) * CW;
+    float* slab = d.partial + ((long long)split * d.T + t0 + 2 * tt) * (long long)d.Cg * d.ncols;
+    const int col = c0 + cc + li;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = wm * WM + 16 * i + 4 * lq + r;
+        slab[(long long)gr * d.ncols + col] = acc[i][j][r];
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+}
+
+template <bool XSQ, int NP = 3>
+__global__ void __launch_bounds__(768, 1) wg_x3p_kernel(const WgDesc d) {
+  constexpr int STAGE = NP * (32 * 192 + 34 * 192);
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+  const int nblk = 25 * d.nsplit;
+  const int b = blockIdx.x;
+  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
+  if (wid >= nblk) return;
+  const int split = wid / 25, rem = wid - (wid / 25) * 25;
+  const int ky = rem / 5, u = rem - (rem / 5) * 5;
+  if (u < 3) wg_x3p_body<XSQ, 3, NP>(d, lds, split, ky, u);
+  else wg_x3p_body<XSQ, 2, NP>(d, lds, split, ky, u - 3);
+}
+
 template <bool XSQ, int NP = 3>
 __global__ void __launch_bounds__(512, 1) wg_x3g_kernel(const WgDesc d) {
   constexpr int STAGE = NP * (32 * 192 + 34 * 192);
@@ -1323,7 +1576,13 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   const bool sq = d.x_op == AOP_SQUARE;
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
-  if (wg_x3g_ok(d)) {
+  if (wg_x3g_ok(d) && WG_X3P) {
+    if (d.bf16) {
+      if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true, 1>), grid, dim3(768), 0, s, d);
+      else hipLaunchKernelGGL((wg_x3p_kernel<false, 1>), grid, dim3(768), 0, s, d);
+    } else if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true>), grid, dim3(768), 0, s, d);
+    else hipLaunchKernelGGL((wg_x3p_kernel<false>), grid, dim3(768), 0, s, d);
+  } else if (wg_x3g_ok(d)) {
     if (d.bf16) {
       if (sq) hipLaunchKernelGGL((wg_x3g_kernel<true, 1>), grid, dim3(512), 0, s, d);
       else hipLaunchKernelGGL((wg_x3g_kernel<false, 1>), grid, dim3(512), 0, s, d);
