@@ -733,7 +733,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #define WG_X3P 1  // the tap-group weight gradients on producer / consumer waves (wg_x3p_kernel); 0: wg_x3g_kernel
 #endif
 #ifndef WG_X3P_PRIO
-#define WG_X3P_PRIO 0  // s_setprio of the producer waves (0: hardware default)
+#define WG_X3P_PRIO 1  // s_setprio of the producer waves (0: hardware default; 1: g_a.2 wgrad 1.163 -> 1.107 ms, r07l)
 #endif
 #ifndef WG_X3P_ABL
 #define WG_X3P_ABL 0  // diagnostic ablations of wg_x3p_kernel (wrong results): 1 no global loads, 2 no LDS stores, 4 no MFMAs, 8 every step loads the split's first pixels (L2-hot), 16 no split (one
