@@ -142,7 +142,8 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
         peak, kern = BF16_PEAK_TFLOPS / 6, ("ig_kernel_x3d (256x192 tiles, operands by LDS-DMA; fp32 by 3-term bf16 "
                                            "split, 16x16x32 bf16 MFMA)")
     elif math == "bf16":
-        peak, kern = BF16_PEAK_TFLOPS, "ig_kernel_bf16<128,192,64,96> (bf16 operands, fp32 accumulation, 32x32x16 bf16 MFMA)"
+        peak, kern = BF16_PEAK_TFLOPS, ("ig_kernel_b16d (256x192 tiles, bf16 operands by LDS-DMA from an NHWC bf16 "
+                                        "copy of the input, fp32 accumulation, 16x16x32 bf16 MFMA)")
     else:
         peak, kern = FP32_PEAK_TFLOPS, "ig_kernel<128,192,64,96> (fp32 MFMA)"
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
@@ -150,7 +151,8 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
             "peak_note": {"fp32_split": "algorithmic fp32 FLOP/s; peak = bf16 dense MFMA 2500 TF / 6 products per fp32 MAC",
                           "bf16": "algorithmic FLOP/s; peak = bf16 dense MFMA spec (2500 TF)"}.get(math, "fp32 dense MFMA spec"),
             "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "kernel": kern + " + weight pack: conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
+            "kernel": kern + (" + weight pack + input bf16 conversion" if math == "bf16" else " + weight pack") +
+                      ": conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4),
             "timing": (f"live: HIP events on the launch stream around the layer's {live_launches} launches "
                        "inside the timed steps" if live_ms else "isolated loop of the same launch"),

@@ -107,6 +107,14 @@ SIGNATURES = {
                               c_void]),
     "ic_gdn_bwd_sum_ex": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_int, c_void, c_size,
                                   c_void]),
+    # bf16 activation copies (config C3): include/imgcomp.h ic_gdn_fwd_xb ... ic_conv_transpose2d_dgrad_xb
+    "ic_gdn_fwd_xb": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_void, c_int, c_void, c_size, c_void]),
+    "ic_gdn_bwd_sum_xb": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_void, c_int,
+                                  c_void, c_size, c_void]),
+    "ic_conv2d_fwd_xb": (c_int, [_ACT, c_void, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int, c_void, c_size,
+                                 c_void]),
+    "ic_conv_transpose2d_dgrad_xb": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size,
+                                             c_void]),
     "ic_nonneg_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void]),
     "ic_nonneg_bwd": (c_int, [c_void, c_void, c_ll, c_float, c_void, c_void]),
     "ic_bound_fwd": (c_int, [c_void, c_ll, c_float, c_int, c_void, c_void]),
@@ -226,7 +234,7 @@ KERNELS = {1: "ig_fp32", 2: "ig_fp32_gather", 3: "ig_bf16", 4: "ig_split", 5: "i
            12: "wg_fp32_gather", 13: "wg_ldsdma", 14: "wg_split", 15: "edge_wgrad", 16: "gdn_fused",
            17: "gdn_fused_split", 18: "gdn_gemm", 20: "wg_bf16",
            21: "gdn_fused_bf16", 22: "ig_split_dma", 23: "edge_conv_bf16", 24: "tconv_few_rows_bf16",
-           25: "edge_wgrad_bf16"}
+           25: "edge_wgrad_bf16", 26: "ig_bf16_dma"}
 
 
 def plan(op, a, b=None, k=1, stride=1, pad=0, math=0):

@@ -160,10 +160,16 @@ int transposed_col2im(const ic_act* x, const float* W, const float* bias, int k,
 }
 
 // y[a] = sum_{t,b} x[b] @ (gy*s + ky - pad) * W[a][b][ky][kx]   (W: [A=y->c][B=x->c][k][k])
+// xb (IC_MATH_XB in math): x's compact NHWC bf16 copy, made by its producer (ic_gdn_fwd_xb /
+// ic_gdn_bwd_sum_xb): the bf16 DMA tiles read it instead of converting x into the workspace (and the
+// workspace query leaves that space out)
 int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
                 const ic_act* y, int epi, int aop, const float* aux0, const float* aux1,
                 const float* aux2, float* aux_out, void* ws, size_t wsb, hipStream_t s, size_t* need,
-                int math = 0) {
+                int math = 0, const void* xb = nullptr) {
+  const bool have_xb = (math & IC_MATH_XB) != 0;
+  math &= ~IC_MATH_XB;
+  if (have_xb && !need && !xb) return IC_ERR_ARG;
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
   if (!act_fits32(x) || !act_fits32(y)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
@@ -196,11 +202,16 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   d.Kc = d.generic ? (int)ic_align((size_t)P.T * x->c, 32) : x->c;
   d.bf16 = (math & IC_MATH_BF16) && !d.generic && x->c % 64 == 0 && aop == AOP_NONE;
   d.x3 = (math & IC_MATH_SPLIT) && !d.bf16 && !d.generic && aop == AOP_NONE;
+  d.b16d_ok = 1;
   const size_t part = ig_plan(d);
   const size_t esz = d.bf16 ? 2 : (d.x3 ? 6 : 4);
   const size_t wpb = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)P.T * d.Npad * x->c * esz;
   d.wplane = (long long)P.T * d.Npad * x->c;
-  const size_t tot = ic_align(wpb, 256) + ic_align(part, 256);
+  // bf16 DMA tiles: the input as a compact NHWC bf16 copy in the workspace (after the pack, which
+  // IC_MATH_WPACKED keeps at the workspace's start)
+  const long long xel = (long long)x->n * x->h * x->w * x->c;
+  const size_t xbb = (d.dma && d.bf16 && !have_xb) ? (size_t)xel * 2 : 0;
+  const size_t tot = ic_align(wpb, 256) + ic_align(part, 256) + ic_align(xbb, 256);
   if (need) {
     plan_report(ig_kernel_kind(d), d.bm, d.bn, d.ksplit, 0, 0, ig_grid_blocks(d));
     *need = tot;
@@ -214,6 +225,16 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
   if (!(math & IC_MATH_WPACKED)) {
     int rc = pack_weights(W, y->c, x->c, k, 0, d.generic, P.T, ky, kx, d.Npad, d.Kc, wp, s, d.x3 ? 2 : d.bf16);
     if (rc) return rc;
+  }
+  if (d.dma && d.bf16) {
+    if (have_xb) {
+      d.xb = xb;
+    } else {
+      void* xc = cv.take(xbb);
+      int rc = ig_cvt_bf16(x->data, xc, xel, s);
+      if (rc) return rc;
+      d.xb = xc;
+    }
   }
   return ig_run(d, s);
 }
@@ -508,6 +529,11 @@ int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int
 size_t ic_conv2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
   return ic_conv2d_fwd_ws_ex(x, k, stride, pad, y, 0);
 }
+int ic_conv2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const float* b, int k, int stride, int pad,
+                     const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream) {
+  return direct_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, AOP_NONE, nullptr,
+                     nullptr, nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr, math | IC_MATH_XB, xb);
+}
 int ic_conv2d_fwd(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
                   const ic_act* y, int act, void* ws, size_t ws_bytes, void* stream) {
   return ic_conv2d_fwd_ex(x, w, b, k, stride, pad, y, act, 0, ws, ws_bytes, stream);
@@ -575,6 +601,11 @@ int ic_conv_transpose2d_dgrad_ex(const ic_act* dy, const float* w, int k, int st
 }
 size_t ic_conv_transpose2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
   return ic_conv_transpose2d_dgrad_ws_ex(dy, k, stride, pad, dx, 0);
+}
+int ic_conv_transpose2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
+                                 const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream) {
+  return direct_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, AOP_NONE, nullptr, nullptr,
+                     nullptr, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr, math | IC_MATH_XB, dyb);
 }
 int ic_conv_transpose2d_dgrad(const ic_act* dy, const float* w, int k, int stride, int pad,
                               const ic_act* dx, void* ws, size_t ws_bytes, void* stream) {

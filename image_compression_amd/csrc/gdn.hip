@@ -56,9 +56,19 @@ void gemm1x1(IgDesc& d, const ic_act* x, const ic_act* y) {
   d.Kc = d.generic ? (int)ic_align((size_t)x->c, 32) : x->c;
 }
 
+// y (and x) compact NHWC: the layout of the bf16 copies (ic_gdn_fwd_xb / ic_gdn_bwd_sum_xb)
+static bool compact_nhwc(const ic_act* a) {
+  return a->sc == 1 && a->sw == a->c && a->sh == (long long)a->w * a->c && a->sn == (long long)a->h * a->w * a->c &&
+         a->c % 8 == 0;
+}
+
+// yb (non-null): y's compact NHWC bf16 copy as well -- written by the fused bf16 kernel's epilogue, or
+// converted after any other path
 int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inverse,
-                 const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
+                 const ic_act* y, float* norm, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0,
+                 void* yb = nullptr) {
   const long long P = (long long)x->n * x->h * x->w;
+  if (yb && !need && !compact_nhwc(y)) return IC_ERR_ARG;
   // split arithmetic: the fused split kernel (C = 192), else the implicit GEMM
   // (1x1, x^2 squared in the staging, GDN epilogue)
   const bool split = (math & IC_MATH_SPLIT) && x->c % 32 == 0 && x->sc == 1 && x->c >= 64;
@@ -66,8 +76,10 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
   if (!need && (!split || x->c == 192) && gdn_fused_ok(x->data, y->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
       ((uintptr_t)gamma & 15) == 0) {
-    return gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s,
-                         (math & IC_MATH_BF16) && split && x->c == 192 ? 2 : split ? 1 : 0);
+    const int mode = (math & IC_MATH_BF16) && split && x->c == 192 ? 2 : split ? 1 : 0;
+    int rc = gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s, mode, mode == 2 ? yb : nullptr);
+    if (rc || !yb || mode == 2) return rc;
+    return ig_cvt_bf16(y->data, yb, act_numel(y), s);
   }
   IgDesc d = {};
   gemm1x1(d, x, y);
@@ -91,12 +103,26 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
   const int z = 0;
   int rc = pack_weights(gamma, x->c, x->c, 1, 0, d.generic, 1, &z, &z, d.Npad, d.Kc, wp, s, d.x3 ? 2 : 0);
   if (rc) return rc;
-  return ig_run(d, s);
+  rc = ig_run(d, s);
+  if (rc || !yb) return rc;
+  return ig_cvt_bf16(y->data, yb, act_numel(y), s);
 }
 
 int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
-                 size_t* need, int math = 0, float* dxsum = nullptr) {
+                 size_t* need, int math = 0, float* dxsum = nullptr, void* dxb = nullptr);
+
+// dxb: dx's compact NHWC bf16 copy as well (the fused bf16 kernel writes it; any other path converts)
+int gdn_bwd_impl_xb(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                    const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s, int math,
+                    float* dxsum, void* dxb) {
+  if (!compact_nhwc(dx)) return IC_ERR_ARG;
+  return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, wsb, s, nullptr, math, dxsum, dxb);
+}
+
+int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                 const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
+                 size_t* need, int math, float* dxsum, void* dxb) {
   const long long n = act_numel(x);
   const long long P = (long long)x->n * x->h * x->w;
   // fused path: x, dx, norm, dy all NHWC-dense with x's strides; its workspace
@@ -104,9 +130,18 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
   const size_t fused_ws = gdn_bwd_fused_ws(x->c, P);
   if (!need && gdn_fused_ok(x->data, dx->data, norm, x->c, x->sc, x->sw, x->sh, x->sn, x->h, x->w, P) &&
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
-      wsb >= fused_ws)
-    return gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s,
-                         (math & IC_MATH_BF16) && x->c == 192 ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0, dxsum);
+      wsb >= fused_ws) {
+    const int mode = (math & IC_MATH_BF16) && x->c == 192 ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0;
+    int rc = gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s, mode, dxsum,
+                           mode == 2 ? dxb : nullptr);
+    if (rc || !dxb || mode == 2) return rc;
+    return ig_cvt_bf16(dx->data, dxb, act_numel(dx), s);
+  }
+  if (dxb && !need) {  // the general path, then the copy
+    int rc = gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, wsb, s, nullptr, math, dxsum, nullptr);
+    if (rc) return rc;
+    return ig_cvt_bf16(dx->data, dxb, act_numel(dx), s);
+  }
   // q has x's layout
   ic_act qa = *x;
   IgDesc d = {};
@@ -245,6 +280,18 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
                       size_t ws_bytes, void* stream) {
   return gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,
                       math, dxsum);
+}
+int ic_gdn_fwd_xb(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
+                  void* yb, int math, void* ws, size_t ws_bytes, void* stream) {
+  if (!yb) return IC_ERR_ARG;
+  return gdn_fwd_impl(x, gamma, beta, inverse, y, norm, ws, ws_bytes, (hipStream_t)stream, nullptr, math, yb);
+}
+int ic_gdn_bwd_sum_xb(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, void* dxb, int math, void* ws,
+                      size_t ws_bytes, void* stream) {
+  if (!dxb) return IC_ERR_ARG;
+  return gdn_bwd_impl_xb(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, math,
+                         dxsum, dxb);
 }
 
 }  // extern "C"

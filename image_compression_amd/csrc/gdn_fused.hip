@@ -125,6 +125,23 @@ __device__ __forceinline__ void store_tile(float* __restrict__ g, uint32_t m0, u
   }
 }
 
+// the same tile as bf16 (round to nearest even): 8 B per lane
+template <int C, int BM, int NT>
+__device__ __forceinline__ void store_tile_b16(__bf16* __restrict__ g, uint32_t m0, uint32_t P, const float* img,
+                                               int tid) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  constexpr int CH = C / 4;
+  constexpr int QPASS = BM * CH / NT;
+#pragma unroll
+  for (int q = 0; q < QPASS; ++q) {
+    const int pos = tid + NT * q;
+    const int row = pos / CH, lc = pos - (pos / CH) * CH;
+    const floatx4v v = *(const floatx4v*)(img + row * C + ((lc ^ (row & 15)) << 2));
+    if (m0 + row < P)
+      *(u32x2*)(g + (size_t)(m0 + row) * C + lc * 4) = u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])};
+  }
+}
+
 // ============================================================== forward
 // NW = C/32 waves (C=192: 6); wave w owns output channels [32w, 32w+32) of every
 // row of a BM=32-pixel tile.  Two blocks share a CU (72 KB LDS each, three
@@ -268,11 +285,13 @@ __global__ void __launch_bounds__(256, 2)
 //
 // NP = 1 (IC_MATH_BF16, config C3): the same kernel on bf16 operands -- Gamma and x^2 rounded to
 // nearest even, one plane each, one product, fp32 accumulation.
-template <int C, int NP = 3>
+// YB (with NP = 1, config C3): y also as a compact bf16 copy (yb), the A operand of the next conv's
+// bf16 DMA tiles (ig_kernel_b16d), so that conv reads 2 B per element and converts nothing.
+template <int C, int NP = 3, bool YB = false>
 __global__ void __launch_bounds__(768, 1)
     gdn_fwd_x3s_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                        const float* __restrict__ beta, int inverse, float* __restrict__ y,
-                       float* __restrict__ norm, uint32_t P) {
+                       float* __restrict__ norm, uint32_t P, __bf16* __restrict__ yb = nullptr) {
   static_assert(C == 192, "12 waves x 16 channels");
   static_assert(NP == 3 || NP == 1, "split (3 planes) or bf16 (1 plane)");
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
@@ -414,6 +433,7 @@ __global__ void __launch_bounds__(768, 1)
         const size_t o = (size_t)min(m0 + m, P - 1) * C + n;
         y[o] = yv;
         norm[o] = nv;
+        if constexpr (YB) yb[o] = (__bf16)yv;  // round to nearest even
       }
     put(lds + b2 * TILE, pt);
     bx = b1;
@@ -541,11 +561,13 @@ __device__ __forceinline__ void bar_wait_lgkm() {
 // accumulation — group A holds gamma as bf16 16x16x32 B fragments (72 VGPRs) and reads q's
 // A fragments from the fp32 q image (8 channels per lane, rounded in registers); group B runs
 // the quadrant GEMM with one product on single bf16 planes of q and x^2.
-template <int C, bool X3, bool BF = false>
+// XB (with BF): dx also as a compact bf16 copy (dxb), the A operand of the previous transposed conv's
+// input gradient on the bf16 DMA tiles (ig_kernel_b16d).
+template <int C, bool X3, bool BF = false, bool XB = false>
 __global__ void __launch_bounds__(512, 2)
     gdn_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
                          const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
-                         float* __restrict__ slab, uint32_t P) {
+                         float* __restrict__ slab, uint32_t P, __bf16* __restrict__ dxb = nullptr) {
   static_assert(!X3 || C == 192, "split dgamma tiles 192 x 192 as 2 x 2 quadrants of 96");
   static_assert(!BF || X3, "bf16 operands run on the split kernel's layout");
   constexpr int NP = BF ? 1 : 3;  // bf16 planes per operand image
@@ -662,6 +684,7 @@ __global__ void __launch_bounds__(512, 2)
       }
       bar_wait_lgkm();  // B3
       store_tile<C, BM, NTA>(dx, tile * BM, P, gs, tid);
+      if constexpr (XB) store_tile_b16<C, BM, NTA>(dxb, tile * BM, P, gs, tid);
       buf ^= 1;
     }
   } else if constexpr (X3) {
@@ -1215,14 +1238,14 @@ int bwd_grid(long long P) {
   return (int)(ntiles < 256 ? ntiles : 256);
 }
 
-template <int C, bool X3 = false, bool BF = false>
+template <int C, bool X3 = false, bool BF = false, bool XB = false>
 int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
                          float* dx, float* dgamma, float* dbeta, float* dxsum, long long P, float* slab,
-                         hipStream_t s) {
+                         hipStream_t s, void* dxb = nullptr) {
   const int grid = bwd_grid(P);
   if (grid < 1) return IC_OK;
-  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3, BF>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse, dx,
-                     slab, (uint32_t)P);
+  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3, BF, XB>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse,
+                     dx, slab, (uint32_t)P, (__bf16*)dxb);
   IC_CHECK_LAUNCH();
   const int stride = GDN_SLAB(C);
   hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
@@ -1244,12 +1267,15 @@ bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long
 }
 
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
-                  long long P, hipStream_t s, int split) {
+                  long long P, hipStream_t s, int split, void* yb) {
   if (split && C == 192) {  // split: 1 = fp32 by the exact split, 2 = bf16 operands (config C3)
     const long long ntiles = (P + 31) / 32;
     const long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
     if (grid < 1) return IC_OK;
-    if (split == 2)
+    if (split == 2 && yb)
+      hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1, true>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta,
+                         inverse, y, norm, (uint32_t)P, (__bf16*)yb);
+    else if (split == 2)
       hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta, inverse,
                          y, norm, (uint32_t)P);
     else
@@ -1272,8 +1298,12 @@ size_t gdn_bwd_fused_ws(int C, long long P) {
 }
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
-                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum) {
+                  float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum,
+                  void* dxb) {
   float* slab = (float*)ws;
+  if (split == 2 && C == 192 && dxb)
+    return gdn_bwd_fused_launch<192, true, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab,
+                                                       s, dxb);
   if (split == 2 && C == 192)
     return gdn_bwd_fused_launch<192, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   if (split && C == 192 && GDN_BWD_X3W) {

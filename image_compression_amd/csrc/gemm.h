@@ -59,12 +59,16 @@ struct IgDesc {
   int x3;            // fp32 by exact three-term bf16 split (fast path, Cin % 32 == 0); wp holds three
                      // bf16 planes [part][t][Npad][Cin], part p at wp + p * wplane (bf16 elements)
   long long wplane;
+  const void* xb;    // with bf16 && dma: x as compact NHWC bf16 (ig_kernel_b16d's A operand), same element offsets
+  int b16d_ok;       // the caller provides xb when ig_plan picks the bf16 DMA tiles (direct_impl)
   IgPhase ph[IC_MAXPH];
 };
 
 // Fill tile choice, mtiles, split-K; returns partial-buffer bytes needed.
 size_t ig_plan(IgDesc& d);
 int ig_run(IgDesc& d, hipStream_t s);
+// x (compact NHWC fp32, n elements, n % 8 == 0) -> xb (bf16, round to nearest even)
+int ig_cvt_bf16(const float* x, void* xb, long long n, hipStream_t s);
 // IC_KERNEL_* that ig_run launches for a planned descriptor, and its grid size
 int ig_kernel_kind(const IgDesc& d);
 long long ig_grid_blocks(const IgDesc& d);
@@ -154,12 +158,14 @@ int col2im_run(const float* ycol, int ncol, int N, int Hi, int Wi, const float* 
 bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long long sc, long long sw, long long sh,
                   long long sn, int H, int W, long long P);
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
-                  long long P, hipStream_t s, int split = 0);  // split: C = 192 in split arithmetic
+                  long long P, hipStream_t s, int split = 0,  // split: C = 192 in split arithmetic
+                  void* yb = nullptr);                         // with split 2 (bf16): y's bf16 copy too
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0,
-                  float* dxsum = nullptr);  // split: 1 split dgamma, 2 bf16 operands in both GEMMs (C = 192);
-                                            // dxsum: column sums of dx over all pixels (C), when non-null
+                  float* dxsum = nullptr,   // split: 1 split dgamma, 2 bf16 operands in both GEMMs (C = 192);
+                  void* dxb = nullptr);     // dxsum: column sums of dx over all pixels (C), when non-null;
+                                            // dxb (split 2): dx's bf16 copy too
 
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,

@@ -932,6 +932,147 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
 }
 
+// bf16 operands on 256 x 192 DMA tiles (C3, round 5): ig_kernel_x3d's block, waves, DMA pipeline and
+// epilogue with both operands already bf16 in HBM -- the activations as a compact NHWC bf16 copy (d.xb)
+// and one packed bf16 weight plane -- so nothing is converted or staged through registers.  K chunks of
+// 64 channels of one tap: 128-B rows for both operands (A 32 KB + B 24 KB per stage, two stages), the
+// 16-B pieces XOR-swizzled by row bits 1-3 (ig_swb: conflict-free ds_read_b128 fragments), two K steps
+// of v_mfma_f32_16x16x32_bf16 per chunk.  Round 3 ran bf16 products on ig_kernel_x3d's fp32-A DMA tiles
+// and was slower than ig_kernel_bf16 (the fp32 A bytes per MAC were six times the split kernel's).
+#ifndef IG_B16D
+#define IG_B16D 1
+#endif
+__device__ __forceinline__ int ig_swb(int r) { return (r >> 1) & 7; }
+
+__global__ void __launch_bounds__(512, 1) ig_kernel_b16d(const IgDesc d) {
+  constexpr int BM = 256, BN = 192, WM = 32, WN = 192, TM = WM / 16, TN = WN / 16;
+  constexpr int ASTAGE = BM * 128;  // 32 KB: 256 rows x 64 bf16
+  constexpr int BSTAGE = BN * 128;  // 24 KB: 192 rows x 64 bf16
+  constexpr int STAGE = ASTAGE + BSTAGE;
+  constexpr int NB = BN / 8;        // 1-KB B pieces per stage (24)
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int T = P.T;
+  const int nchunks = T * (d.Cin >> 6);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+
+  // A: wave w DMAs rows 32w + 8k + (lane >> 3), k < 4; lane's physical piece lane & 7 holds logical
+  // piece (lane & 7) ^ ig_swb(row) (offsets in bf16 elements)
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[4];
+  int a_iy[4], a_ix[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = 32 * w + 8 * k + (lane >> 3);
+    const uint32_t m = m0 + row;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[k] = (int)gx * d.stride;
+    a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
+               8u * (uint32_t)((lane & 7) ^ ig_swb(row & 15));
+  }
+  // B: wave w DMAs pieces jj = w + 8 kb < 24: rows 8 jj + (lane >> 3)
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  uint32_t b_off[3];
+#pragma unroll
+  for (int kb = 0; kb < 3; ++kb) {
+    const int rb = 8 * (w + 8 * kb) + (lane >> 3);
+    b_off[kb] = (uint32_t)rb * (uint32_t)d.Cin + 8u * (uint32_t)((lane & 7) ^ ig_swb(rb & 15));
+  }
+  const __bf16* __restrict__ xg = (const __bf16*)d.xb;
+  auto issue = [&](int cc, int t, int st) {
+    const uint32_t sb = lbase + (uint32_t)(st * STAGE);
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
+                sb + (uint32_t)((4 * w + k) * 1024));
+    }
+    const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 64);
+#pragma unroll
+    for (int kb = 0; kb < 3; ++kb) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (w + 8 * kb) * 1024));
+  };
+  static_assert(NB == 24, "three B pieces per wave");
+
+  const int wm = w, wn = 0;
+  const int r = lane & 15, g = lane >> 4;
+  const int ch0 = 16 * ((g) ^ ig_swb(r)), ch1 = 16 * ((4 + g) ^ ig_swb(r));  // byte offsets of K steps 0, 1
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  const int CC = d.Cin >> 6;
+  int cn = cb / T, tn = cb - (cb / T) * T;  // channel chunk and tap of the next chunk to issue
+  if (cb < ce) {
+    issue(cn, tn, 0);
+    if (++tn == T) { tn = 0; ++cn; }
+  }
+  (void)CC;
+  for (int c = cb; c < ce; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* As = lds + ((c - cb) & 1) * STAGE;
+    const char* Bs = As + ASTAGE;
+    bf16x8 a[2][TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const char* ar = As + (wm * WM + i * 16 + r) * 128;
+      a[0][i] = *(const bf16x8*)(ar + ch0);
+      a[1][i] = *(const bf16x8*)(ar + ch1);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j == IG_X3D_DMA_J && c + 1 < ce) {
+        issue(cn, tn, (c + 1 - cb) & 1);
+        if (++tn == T) { tn = 0; ++cn; }
+      }
+      const char* br = Bs + (wn * WN + j * 16 + r) * 128;
+      const bf16x8 b0 = *(const bf16x8*)(br + ch0);
+      const bf16x8 b1 = *(const bf16x8*)(br + ch1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b0, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b1, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
+}
+
+__global__ void __launch_bounds__(256) ig_cvt_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ xb,
+                                                          long long n8) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const floatx4v lo = *(const floatx4v*)(x + 8 * i), hi = *(const floatx4v*)(x + 8 * i + 4);
+    *(u32x4*)(xb + 8 * i) = u32x4{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3]),
+                                  ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])};
+  }
+}
+
 // split-K reduction + epilogue: one thread per (row, channel)
 __global__ void ig_reduce_kernel(const IgDesc d) {
   const long long total = d.Mtot * d.Cout;
@@ -1036,6 +1177,13 @@ size_t ig_plan(IgDesc& d) {
       // 9 / 6 / 6 / 4 taps, so equal chunk ranges leave one block per CU waiting on the longest
       if (t256 >= 256 || (d.nphase == 1 && t256 >= IG_X3D_MINT)) { d.bm = 256; d.dma = 1; }
     }
+    // bf16 operands on one-phase maps: the DMA tiles (ig_kernel_b16d) on a compact NHWC input
+    if (IG_B16D && d.b16d_ok && d.bf16 && !d.generic && d.Cout == 192 && d.a_op == AOP_NONE && d.nphase == 1 && d.xs_c == 1 &&
+        d.Cin % 64 == 0 && d.xs_w == d.Cin && d.xs_h == (long long)d.Wx * d.Cin &&
+        d.xs_n == (long long)d.Hx * d.Wx * d.Cin) {
+      const long long t256 = ic_cdiv((long long)d.N * d.ph[0].Hg * d.ph[0].Wg, 256);
+      if (t256 >= IG_X3D_MINT) { d.bm = 256; d.dma = 1; }
+    }
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
   else { d.bm = 256; d.bn = 32; }
@@ -1084,7 +1232,7 @@ size_t ig_plan(IgDesc& d) {
 }
 
 int ig_kernel_kind(const IgDesc& d) {
-  if (d.bf16) return ig_bf16_wide(d) ? IC_KERNEL_IG_BF16 : IC_KERNEL_IG_SPLIT_BF16;
+  if (d.bf16) return d.dma ? IC_KERNEL_IG_BF16_DMA : ig_bf16_wide(d) ? IC_KERNEL_IG_BF16 : IC_KERNEL_IG_SPLIT_BF16;
   if (d.x3) return d.dma ? IC_KERNEL_IG_SPLIT_DMA : IC_KERNEL_IG_SPLIT;
   return d.generic ? IC_KERNEL_IG_FP32_GATHER : IC_KERNEL_IG_FP32;
 }
@@ -1106,7 +1254,12 @@ int ig_run(IgDesc& d, hipStream_t s) {
     int mt = 0;
     for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
     if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
-    hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+    if (d.bf16) {
+      if (!d.xb || d.nphase != 1 || d.Cin % 64 != 0) return IC_ERR_ARG;
+      hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.ksplit), dim3(512), 0, s, d);
+    } else {
+      hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+    }
     IC_CHECK_LAUNCH();
     rc = IC_OK;
   }
@@ -1122,5 +1275,16 @@ int ig_run(IgDesc& d, hipStream_t s) {
     hipLaunchKernelGGL(ig_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d);
     IC_CHECK_LAUNCH();
   }
+  return IC_OK;
+}
+
+int ig_cvt_bf16(const float* x, void* xb, long long n, hipStream_t s) {
+  if (n % 8 != 0) return IC_ERR_ARG;
+  const long long n8 = n / 8;
+  long long blocks = (n8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) return IC_OK;
+  hipLaunchKernelGGL(ig_cvt_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, (__bf16*)xb, n8);
+  IC_CHECK_LAUNCH();
   return IC_OK;
 }

@@ -288,6 +288,91 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum(const Tensor& x, const Te
 }
 
 
+// ---------------------------------------------------------------- bf16 activation copies (C3)
+// The GDN output / input gradient also as a bf16 tensor of the same shape and strides (compact NHWC),
+// and the conv forward / transposed-conv input gradient that reads such a copy (include/imgcomp.h
+// ic_gdn_fwd_xb, ic_gdn_bwd_sum_xb, ic_conv2d_fwd_xb, ic_conv_transpose2d_dgrad_xb).
+void check_copy(const Tensor& b, const Tensor& like, const char* what) {
+  TORCH_CHECK(b.is_cuda() && b.scalar_type() == at::kBFloat16 && b.sizes() == like.sizes() &&
+                  b.strides() == like.strides(),
+              "imgcomp: ", what, " must be a bf16 tensor with the shape and strides of its fp32 tensor");
+}
+std::tuple<Tensor, Tensor, Tensor> gdn_fwd_xb(const Tensor& x, const Tensor& gamma, const Tensor& beta, bool inverse,
+                                              int64_t math) {
+  check_operand(x, "x");
+  check_operand(gamma, "gamma");
+  check_operand(beta, "beta");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(gamma.numel() == x.size(1) * x.size(1) && beta.numel() == x.size(1), "gdn: parameters do not match ",
+              x.sizes());
+  Tensor y = at::empty_like(x);
+  Tensor norm = at::empty_like(x);
+  Tensor yb = at::empty_like(x, x.options().dtype(at::kBFloat16));
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb = ic_gdn_fwd_ws_ex(&ax, (int)math);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_gdn_fwd_xb(&ax, gamma.data_ptr<float>(), beta.data_ptr<float>(), inverse ? 1 : 0, &ay,
+                         norm.data_ptr<float>(), yb.data_ptr(), (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "gdn_fwd_xb");
+  return {y, norm, yb};
+}
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_xb(const Tensor& x, const Tensor& norm, const Tensor& dy,
+                                                                  const Tensor& gamma, bool inverse, int64_t math) {
+  check_operand(x, "x");
+  check_operand(dy, "dy");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "gdn_bwd_sum_xb: dy must have x's shape and strides");
+  Tensor dx = at::empty_like(x);
+  Tensor dg = at::empty_like(gamma, at::MemoryFormat::Contiguous);
+  Tensor dbeta = at::empty({x.size(1)}, gamma.options());
+  Tensor dxsum = at::empty({x.size(1)}, gamma.options());
+  Tensor dxb = at::empty_like(x, x.options().dtype(at::kBFloat16));
+  const ic_act ax = act_of(x), adx = act_of(dx);
+  const size_t nb = ic_gdn_bwd_ws(&ax);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_gdn_bwd_sum_xb(&ax, norm.data_ptr<float>(), dy.data_ptr<float>(), gamma.data_ptr<float>(),
+                             inverse ? 1 : 0, &adx, dg.data_ptr<float>(), dbeta.data_ptr<float>(),
+                             dxsum.data_ptr<float>(), dxb.data_ptr(), (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "gdn_bwd_sum_xb");
+  return {dx, dg, dbeta, dxsum, dxb};
+}
+Tensor conv2d_fwd_xb(const Tensor& x, const Tensor& xb, const Tensor& w, const c10::optional<Tensor>& b, int64_t stride,
+                     int64_t pad, int64_t act, int64_t math) {
+  check_operand(x, "x");
+  check_operand(w, "weight");
+  check_copy(xb, x, "xb");
+  if (b.has_value()) check_operand(*b, "bias");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == w.size(3), "conv2d: weight ", w.sizes(),
+              " does not match input ", x.sizes());
+  const int64_t k = w.size(2);
+  const int64_t ho = (x.size(2) + 2 * pad - k) / stride + 1, wo = (x.size(3) + 2 * pad - k) / stride + 1;
+  Tensor y = new_act(x, x.size(0), w.size(0), ho, wo);
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb = ic_conv2d_fwd_ws_ex(&ax, (int)k, (int)stride, (int)pad, &ay, (int)math | IC_MATH_XB);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_conv2d_fwd_xb(&ax, xb.data_ptr(), w.data_ptr<float>(), opt_ptr(b), (int)k, (int)stride, (int)pad, &ay,
+                            (int)act, (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "conv2d_fwd_xb");
+  return y;
+}
+Tensor conv_transpose2d_dgrad_xb(const Tensor& dy, const Tensor& dyb, const Tensor& w, const Tensor& x, int64_t stride,
+                                 int64_t pad, int64_t math) {
+  check_operand(dy, "dy");
+  check_operand(w, "weight");
+  check_copy(dyb, dy, "dyb");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dx = new_act(dy, x.size(0), x.size(1), x.size(2), x.size(3));
+  const ic_act ag = act_of(dy), adx = act_of(dx);
+  const int k = (int)w.size(2);
+  const size_t nb = ic_conv_transpose2d_dgrad_ws_ex(&ag, k, (int)stride, (int)pad, &adx, (int)math | IC_MATH_XB);
+  Tensor ws = workspace(dy, nb);
+  check_rc(ic_conv_transpose2d_dgrad_xb(&ag, dyb.data_ptr(), w.data_ptr<float>(), k, (int)stride, (int)pad, &adx,
+                                        (int)math, ws.data_ptr(), nb, stream_of(dy)),
+           "conv_transpose2d_dgrad_xb");
+  return dx;
+}
+
 // ---------------------------------------------------------------- elementwise, losses, entropy models
 // Reference interfaces: NonNegativeParam.forward (layers/gdn.py:59-62), Lower/UpperBound
 // (layers/bound.py:28-59), ReLU / torch.abs (prior_analysis.py:65, bmshl2018.py:72), the exp-clamp of
@@ -787,6 +872,23 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_meta(const Tensor& x, con
 }
 
 
+std::tuple<Tensor, Tensor, Tensor> gdn_fwd_xb_meta(const Tensor& x, const Tensor&, const Tensor&, bool, int64_t) {
+  return {at::empty_like(x), at::empty_like(x), at::empty_like(x, x.options().dtype(at::kBFloat16))};
+}
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_xb_meta(const Tensor& x, const Tensor&, const Tensor&,
+                                                                       const Tensor& gamma, bool, int64_t) {
+  return {at::empty_like(x), at::empty_like(gamma, at::MemoryFormat::Contiguous), at::empty({x.size(1)}, gamma.options()),
+          at::empty({x.size(1)}, gamma.options()), at::empty_like(x, x.options().dtype(at::kBFloat16))};
+}
+Tensor conv2d_fwd_xb_meta(const Tensor& x, const Tensor&, const Tensor& w, const c10::optional<Tensor>& b,
+                          int64_t stride, int64_t pad, int64_t act, int64_t math) {
+  return conv2d_fwd_meta(x, w, b, stride, pad, act, math);
+}
+Tensor conv_transpose2d_dgrad_xb_meta(const Tensor& dy, const Tensor&, const Tensor& w, const Tensor& x, int64_t s,
+                                      int64_t p, int64_t m) {
+  return conv_transpose2d_dgrad_meta(dy, w, x, s, p, m);
+}
+
 // elementwise / loss / entropy shape kernels
 Tensor like_meta1(const Tensor& x) { return at::empty_like(x, at::MemoryFormat::Preserve); }
 Tensor nonneg_fwd_meta(const Tensor& p, double, double) { return like_meta1(p); }
@@ -885,6 +987,13 @@ TORCH_LIBRARY(imgcomp, m) {
   m.def("gdn_bwd(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> (Tensor, Tensor, Tensor)");
   m.def("gdn_bwd_sum(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> "
         "(Tensor, Tensor, Tensor, Tensor)");
+  m.def("gdn_fwd_xb(Tensor x, Tensor gamma, Tensor beta, bool inverse, int math) -> (Tensor, Tensor, Tensor)");
+  m.def("gdn_bwd_sum_xb(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> "
+        "(Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("conv2d_fwd_xb(Tensor x, Tensor xb, Tensor weight, Tensor? bias, int stride, int padding, int act, "
+        "int math) -> Tensor");
+  m.def("conv_transpose2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, "
+        "int math) -> Tensor");
   m.def("nonneg_fwd(Tensor p, float bound, float pedestal) -> Tensor");
   m.def("nonneg_bwd(Tensor p, Tensor grad, float bound) -> Tensor");
   m.def("nonneg_multi_fwd(Tensor[] p, float[] bound, float[] pedestal) -> Tensor[]");
@@ -935,6 +1044,10 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("gdn_fwd", gdn_fwd);
   m.impl("gdn_bwd", gdn_bwd);
   m.impl("gdn_bwd_sum", gdn_bwd_sum);
+  m.impl("gdn_fwd_xb", gdn_fwd_xb);
+  m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb);
+  m.impl("conv2d_fwd_xb", conv2d_fwd_xb);
+  m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb);
   m.impl("nonneg_fwd", nonneg_fwd);
   m.impl("nonneg_bwd", nonneg_bwd);
   m.impl("nonneg_multi_fwd", nonneg_multi_fwd);
@@ -977,6 +1090,10 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("gdn_fwd", gdn_fwd_meta);
   m.impl("gdn_bwd", gdn_bwd_meta);
   m.impl("gdn_bwd_sum", gdn_bwd_sum_meta);
+  m.impl("gdn_fwd_xb", gdn_fwd_xb_meta);
+  m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb_meta);
+  m.impl("conv2d_fwd_xb", conv2d_fwd_xb_meta);
+  m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb_meta);
   m.impl("nonneg_fwd", nonneg_fwd_meta);
   m.impl("nonneg_bwd", nonneg_bwd_meta);
   m.impl("nonneg_multi_fwd", nonneg_multi_fwd_meta);

@@ -118,6 +118,37 @@ def _take_colsum(t):
     return s if (r() is t and t._version == ver) else None
 
 
+# ---------------------------------------------------------- bf16 activation copies (config C3)
+# A GDN whose output feeds a conv forward on the bf16 DMA tiles (GDN.xb & 1), or whose input
+# gradient feeds a transposed conv's input gradient there (GDN.xb & 2), writes that tensor's compact
+# NHWC bf16 copy in the same kernel (torch.ops.imgcomp.gdn_fwd_xb / gdn_bwd_sum_xb) and leaves it
+# here, keyed like the column sums above; the consuming conv takes it (conv2d_fwd_xb /
+# conv_transpose2d_dgrad_xb) and reads 2 B per element instead of converting the fp32 tensor.
+_BF16 = {}
+_BF16_LOCK = threading.Lock()
+BF16_COPY_STATS = {"put": 0, "hit": 0}
+
+
+def _put_bf16(t, tb):
+    with _BF16_LOCK:
+        for k in [k for k, (r, _, _) in _BF16.items() if r() is None]:
+            del _BF16[k]
+        _BF16[_colsum_key(t)] = (weakref.ref(t), t._version, tb)
+        BF16_COPY_STATS["put"] += 1
+
+
+def _take_bf16(t):
+    with _BF16_LOCK:
+        e = _BF16.pop(_colsum_key(t), None)
+    if e is None:
+        return None
+    r, ver, tb = e
+    if r() is t and t._version == ver and tb.shape == t.shape and tb.stride() == t.stride():
+        BF16_COPY_STATS["hit"] += 1
+        return tb
+    return None
+
+
 class Conv2dFn(Function):
     """torch.nn.Conv2d forward/backward (analysis.py:55, prior_analysis.py:54-56), each
     launch one torch.ops.imgcomp op (csrc/torch_ops.cpp -> C ABI)."""
@@ -130,7 +161,11 @@ class Conv2dFn(Function):
         b = None if bias is None else bias.contiguous()
         if w.shape[1] != x.shape[1] or w.shape[2] != w.shape[3]:
             raise RuntimeError(f"conv2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
-        y = _lib.ops().conv2d_fwd(x, w, b, stride, padding, int(act), int(math))
+        xb = _take_bf16(x) if int(math) & MATH["bf16"] else None
+        if xb is not None:
+            y = _lib.ops().conv2d_fwd_xb(x, xb, w, b, stride, padding, int(act), int(math))
+        else:
+            y = _lib.ops().conv2d_fwd(x, w, b, stride, padding, int(act), int(math))
         _log_plan("conv2d_fwd", x, y, w.shape[2], stride, padding, math)
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
@@ -180,12 +215,16 @@ class ConvTranspose2dFn(Function):
         stride, padding, act, has_b, math = ctx.conf
         # the bias gradient formed by gy's producer (taken only where this node owns the bias gradient)
         pre = _take_colsum(gy) if (has_b and not act and ctx.needs_input_grad[2]) else None
+        gyb = _take_bf16(gy) if (math & MATH["bf16"]) and not act else None
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
         dx = dw = db = None
         ops, k = _lib.ops(), w.shape[2]
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and gyb is not None and gyb.stride() == gy.stride():
+            dx = ops.conv_transpose2d_dgrad_xb(gy, gyb, w, x, stride, padding, math)
+            _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
+        elif ctx.needs_input_grad[0]:
             dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
@@ -412,15 +451,22 @@ class GDNFn(Function):
     """modelling/layers/gdn.py:84-86 given re-parameterised gamma (C,C,1,1), beta (C,)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, inverse, math=0, math_fwd=0):
+    def forward(ctx, x, gamma, beta, inverse, math=0, math_fwd=0, xb=0):
         _lib.require_device(x, gamma, beta)
         x = _cl(x)
         g = gamma.contiguous()
         b = beta.contiguous()
-        y, norm = _lib.ops().gdn_fwd(x, g, b, bool(inverse), int(math_fwd))
+        # xb & 1: y's bf16 copy for the next conv's forward; xb & 2: dx's for the previous
+        # transposed conv's input gradient (bf16 operands only; see _put_bf16)
+        if (xb & 1) and (int(math_fwd) & MATH["bf16"]):
+            y, norm, yb = _lib.ops().gdn_fwd_xb(x, g, b, bool(inverse), int(math_fwd))
+            _put_bf16(y, yb)
+        else:
+            y, norm = _lib.ops().gdn_fwd(x, g, b, bool(inverse), int(math_fwd))
         _log_plan("gdn_fwd", x, None, math=math_fwd)
         ctx.inverse = bool(inverse)
         ctx.math = int(math)
+        ctx.xb = int(xb)
         ctx.save_for_backward(x, norm, g)
         return y
 
@@ -430,16 +476,21 @@ class GDNFn(Function):
         gy = _match(gy, x)
         # dx's column sums come with it (the fused backward forms them from its dx tiles): the
         # bias gradient of the conv that produced x, taken by that conv's backward (_take_colsum)
-        dx, dg, dbeta, dxsum = _lib.ops().gdn_bwd_sum(x, norm, gy, g, ctx.inverse, ctx.math)
+        if (ctx.xb & 2) and (ctx.math & MATH["bf16"]):
+            dx, dg, dbeta, dxsum, dxb = _lib.ops().gdn_bwd_sum_xb(x, norm, gy, g, ctx.inverse, ctx.math)
+            _put_bf16(dx, dxb)
+        else:
+            dx, dg, dbeta, dxsum = _lib.ops().gdn_bwd_sum(x, norm, gy, g, ctx.inverse, ctx.math)
         _put_colsum(dx, dxsum)
         _log_plan("gdn_bwd", x, None, math=ctx.math)
-        return dx, dg, dbeta, None, None, None
+        return dx, dg, dbeta, None, None, None, None
 
 
-def gdn(x, gamma, beta, inverse=False, math=0, math_fwd=0):
+def gdn(x, gamma, beta, inverse=False, math=0, math_fwd=0, xb=0):
     """`math` 2: the backward's dgamma GEMM in split arithmetic (C = 192); `math_fwd` 2: the
-    forward on the split implicit GEMM instead of the fused fp32 kernel."""
-    return GDNFn.apply(x, gamma, beta, bool(inverse), int(math), int(math_fwd))
+    forward on the split implicit GEMM instead of the fused fp32 kernel; `xb`: bf16 copies of the
+    output (1) / input gradient (2) for the neighbouring conv (bf16 operands, see _put_bf16)."""
+    return GDNFn.apply(x, gamma, beta, bool(inverse), int(math), int(math_fwd), int(xb))
 
 
 class NonNegFn(Function):

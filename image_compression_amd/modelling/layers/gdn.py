@@ -35,6 +35,8 @@ class NonNegativeParam(nn.Module):
 class GDN(nn.Module):
     math = 0       # IC_MATH_*: 2 forms the backward's dgamma in split arithmetic (C = 192; set_compute_dtype)
     math_fwd = 0   # IC_MATH_*: 2 runs the forward in split arithmetic (fused kernel at C = 192; set_compute_dtype)
+    xb = 0         # bf16 operands (C3): 1 writes y's bf16 copy for the next conv, 2 dx's for the previous
+                   # transposed conv's input gradient (functional._put_bf16; set_compute_dtype)
 
     def __init__(self, in_channels, inverse=False, relu=False,
                  gamma_init=0.1, beta_min=1e-6, offset=2 ** -18):
@@ -50,4 +52,5 @@ class GDN(nn.Module):
     def forward(self, x):
         if self.relu:
             x = ReLUFn.apply(x)
-        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse), int(self.math), int(self.math_fwd))
+        return GDNFn.apply(x, self.gamma(), self.beta(), bool(self.inverse), int(self.math), int(self.math_fwd),
+                           int(self.xb))

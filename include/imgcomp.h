@@ -102,6 +102,10 @@ int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stri
  *      (the im2col fallback, the row-stationary transposed edge) ignore it.  The caller owns the invalidation: any change of
  *      the weight needs a forward without the flag first. */
 #define IC_MATH_WPACKED 4
+/*      IC_MATH_XB (or-ed into IC_MATH_BF16, in the workspace query of a conv forward / transposed-conv
+ *      input gradient whose caller passes the input's bf16 copy to ic_conv2d_fwd_xb /
+ *      ic_conv_transpose2d_dgrad_xb): the workspace leaves out the space the conversion of x would take. */
+#define IC_MATH_XB 8
 size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
 int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
                      const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
@@ -157,6 +161,23 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
                       const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, int math, void* ws,
                       size_t ws_bytes, void* stream);
 
+/* ---- bf16 activation copies (config C3, round 5): a GDN forward / backward whose output feeds a
+ *      192 -> 192 conv forward / transposed-conv input gradient on the bf16 DMA tiles also writes that
+ *      output as a compact NHWC bf16 copy (round to nearest even: the operand the conv would form);
+ *      the conv reads the copy (2 B per element, nothing converted).  y / dx must be compact NHWC
+ *      (channel stride 1), C % 8 == 0.  Replace (reference modelling/layers/gdn.py:79-88 feeding
+ *      modelling/blocks/analysis.py:55, synthesis.py:55-57) the plain forms above. */
+int ic_gdn_fwd_xb(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, float* norm,
+                  void* yb, int math, void* ws, size_t ws_bytes, void* stream);
+int ic_gdn_bwd_sum_xb(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, void* dxb, int math, void* ws,
+                      size_t ws_bytes, void* stream);
+/* xb / dyb: the input's bf16 copy (NULL is an error; the workspace from *_ws_ex with math | IC_MATH_XB) */
+int ic_conv2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const float* b, int k, int stride, int pad,
+                     const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
+int ic_conv_transpose2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
+                                 const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- launch-plan query: which kernel instance, tile and K / pixel split a conv or GDN op would launch
  *      for these shapes (no launch, no device access; the same decision code as the launching entry
  *      points).  op selects the entry point and the meaning of (a, b):
@@ -202,6 +223,7 @@ int ic_gdn_bwd_sum_ex(const ic_act* x, const float* norm, const float* dy, const
 #define IC_KERNEL_EDGE_CONV_BF16 23 /* edge_conv_x3_kernel with bf16 operands (one product), fp32 accumulation */
 #define IC_KERNEL_TCONV_FEW_ROWS_BF16 24 /* tconv_few2_kernel with bf16 operands (one product) */
 #define IC_KERNEL_EDGE_WGRAD_BF16 25 /* edge_wgrad_kernel with bf16 operands (one product) */
+#define IC_KERNEL_IG_BF16_DMA 26    /* ig_kernel_b16d: bf16 operands, 256-row tiles, operands by LDS-DMA (C3) */
 typedef struct ic_plan {
   int kernel;        /* IC_KERNEL_* of the main launch */
   int bm, bn;        /* block tile: output rows (pixels; weight-gradient: G channels) x columns */

@@ -127,7 +127,7 @@ def check_relu_ties(masks, ctl, tau=1e-4):
 
 
 BF16_KERNELS = ("ig_bf16", "ig_split_bf16", "wg_bf16", "gdn_fused_bf16", "edge_conv_bf16", "tconv_few_rows_bf16",
-                "edge_wgrad_bf16")
+                "edge_wgrad_bf16", "ig_bf16_dma")
 
 
 def edges_bf16():

@@ -171,7 +171,12 @@ def test_plan_query_c2_instances():
     p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 0)
     assert p["kernel"] == "ig_fp32"
     p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 1)
-    assert p["kernel"] == "ig_bf16"
+    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_bf16_dma", 256, 1)
+    # bf16 operands: a transposed conv's phases stay on ig_kernel_bf16 (the DMA tiles are one-phase)
+    p = _lib.plan("conv2d_dgrad", y, x, 5, 2, 2, 1)
+    assert (p["kernel"], p["bm"]) == ("ig_bf16", 128)
+    p = _lib.plan("conv_transpose2d_dgrad", x, y, 5, 2, 2, 1)
+    assert (p["kernel"], p["bm"]) == ("ig_bf16_dma", 256)
     # small maps: 64-row tiles with split-K
     p = _lib.plan("conv2d_fwd", _act(32, 192, 16, 16), _act(32, 192, 8, 8), 5, 2, 2, 2)
     assert (p["kernel"], p["bm"]) == ("ig_split", 64) and p["ksplit"] > 1
@@ -311,6 +316,14 @@ def _meta_cases():
         "gdn_bwd": (lambda o: o.gdn_bwd(x, x, x, _meta(192, 192), False, 2), [s, (192, 192), (192,)]),
         "gdn_bwd_sum": (lambda o: o.gdn_bwd_sum(x, x, x, _meta(192, 192), False, 2),
                         [s, (192, 192), (192,), (192,)]),
+        "gdn_fwd_xb": (lambda o: o.gdn_fwd_xb(x, _meta(192, 192), _meta(192), False, 3), [s, s, s]),
+        "gdn_bwd_sum_xb": (lambda o: o.gdn_bwd_sum_xb(x, x, x, _meta(192, 192), False, 3),
+                           [s, (192, 192), (192,), (192,), s]),
+        "conv2d_fwd_xb": (lambda o: o.conv2d_fwd_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5),
+                                                    None, 2, 2, 0, 3), [(2, 192, 8, 8)]),
+        "conv_transpose2d_dgrad_xb": (lambda o: o.conv_transpose2d_dgrad_xb(
+            x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5), _meta(2, 192, 8, 8, cl=True), 2, 2, 3),
+                                      [(2, 192, 8, 8)]),
     }
 
 
