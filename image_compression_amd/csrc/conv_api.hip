@@ -240,8 +240,13 @@ int direct_impl(const ic_act* x, const float* W, const float* bias, int k, int s
 }
 
 // y[b] at (s*iy - pad + ky) += x[a] @ iy * W[a][b][ky][kx]    (W: [A=x->c][B=y->c][k][k])
+// xb (IC_MATH_XB): as direct_impl -- x's bf16 copy for the bf16 DMA tiles of the phases
 int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, int stride, int pad,
-                    const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
+                    const ic_act* y, int epi, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0,
+                    const void* xb = nullptr) {
+  const bool have_xb = (math & IC_MATH_XB) != 0;
+  math &= ~IC_MATH_XB;
+  if (have_xb && !need && !xb) return IC_ERR_ARG;
   if (k < 1 || k * k > IC_MAXT || stride < 1 || stride > 2) return IC_ERR_ARG;
   if (x->n != y->n) return IC_ERR_ARG;
   if (!act_fits32(x) || !act_fits32(y)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
@@ -302,6 +307,7 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   int ttot = 0;
   for (int p = 0; p < np; ++p) ttot += d.ph[p].T;
   d.x3 = (math & IC_MATH_SPLIT) && !d.bf16 && !d.generic && ttot <= IC_MAXT;
+  d.b16d_ok = ttot <= IC_MAXT;  // the bf16 DMA tiles need the one-launch pack of every phase (below)
   const size_t part = ig_plan(d);
   if (d.x3) {
     // one pack of three bf16 planes [part][t over all phases][Npad][Cin]
@@ -335,6 +341,9 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
     wpb[p] = d.generic ? (size_t)d.Npad * d.Kc * 4 : (size_t)d.ph[p].T * d.Npad * x->c * (d.bf16 ? 2 : 4);
     tot += ic_align(wpb[p], 256);
   }
+  const long long xel = (long long)x->n * x->h * x->w * x->c;
+  const size_t xbb = (d.dma && d.bf16 && !have_xb) ? (size_t)xel * 2 : 0;
+  tot += ic_align(xbb, 256);
   if (need) {
     plan_report(ig_kernel_kind(d), d.bm, d.bn, d.ksplit, 0, 0, ig_grid_blocks(d));
     *need = tot;
@@ -343,10 +352,21 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
   if (wsb < tot) return IC_ERR_WORKSPACE;
   Carve cv{(char*)ws, 0};
   d.partial = part ? cv.take(part) : nullptr;
+  if (d.dma && d.bf16) {  // the bf16 DMA tiles' A operand: the caller's copy, or x converted here
+    if (have_xb) {
+      d.xb = xb;
+    } else {
+      void* xc = cv.take(xbb);
+      int rc = ig_cvt_bf16(x->data, xc, xel, s);
+      if (rc) return rc;
+      d.xb = xc;
+    }
+  }
   // fast layout: the phases' [t][n][r] packs are back to back in the
   // workspace (each a multiple of 256 B), so one launch packs every phase
   bool contiguous = !d.generic;
   for (int p = 0; p < np; ++p) contiguous = contiguous && wpb[p] % 256 == 0;
+  if (d.dma && !(contiguous && ttot <= IC_MAXT)) return IC_ERR_ARG;
   if (contiguous && ttot <= IC_MAXT) {
     int aky[IC_MAXT], akx[IC_MAXT], t0 = 0;
     for (int p = 0; p < np; ++p) {
@@ -550,6 +570,11 @@ int ic_conv2d_dgrad_ex(const ic_act* dy, const float* w, int k, int stride, int 
   return transposed_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, ws, ws_bytes,
                          (hipStream_t)stream, nullptr, math);
 }
+int ic_conv2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
+                       const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream) {
+  return transposed_impl(dy, w, nullptr, k, stride, pad, dx, EPI_NONE, ws, ws_bytes, (hipStream_t)stream, nullptr,
+                         math | IC_MATH_XB, dyb);
+}
 size_t ic_conv2d_dgrad_ws(const ic_act* dy, int k, int stride, int pad, const ic_act* dx) {
   return ic_conv2d_dgrad_ws_ex(dy, k, stride, pad, dx, 0);
 }
@@ -577,6 +602,11 @@ int ic_conv_transpose2d_fwd_ex(const ic_act* x, const float* w, const float* b, 
                                const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream) {
   return transposed_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, ws, ws_bytes,
                          (hipStream_t)stream, nullptr, math);
+}
+int ic_conv_transpose2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const float* b, int k, int stride,
+                               int pad, const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream) {
+  return transposed_impl(x, w, b, k, stride, pad, y, act ? EPI_RELU : EPI_NONE, ws, ws_bytes, (hipStream_t)stream,
+                         nullptr, math | IC_MATH_XB, xb);
 }
 size_t ic_conv_transpose2d_fwd_ws(const ic_act* x, int k, int stride, int pad, const ic_act* y) {
   return ic_conv_transpose2d_fwd_ws_ex(x, k, stride, pad, y, 0);

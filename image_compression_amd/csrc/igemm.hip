@@ -1178,11 +1178,13 @@ size_t ig_plan(IgDesc& d) {
       if (t256 >= 256 || (d.nphase == 1 && t256 >= IG_X3D_MINT)) { d.bm = 256; d.dma = 1; }
     }
     // bf16 operands on one-phase maps: the DMA tiles (ig_kernel_b16d) on a compact NHWC input
-    if (IG_B16D && d.b16d_ok && d.bf16 && !d.generic && d.Cout == 192 && d.a_op == AOP_NONE && d.nphase == 1 && d.xs_c == 1 &&
+    if (IG_B16D && d.b16d_ok && d.bf16 && !d.generic && d.Cout == 192 && d.a_op == AOP_NONE && d.xs_c == 1 &&
         d.Cin % 64 == 0 && d.xs_w == d.Cin && d.xs_h == (long long)d.Wx * d.Cin &&
         d.xs_n == (long long)d.Hx * d.Wx * d.Cin) {
-      const long long t256 = ic_cdiv((long long)d.N * d.ph[0].Hg * d.ph[0].Wg, 256);
-      if (t256 >= IG_X3D_MINT) { d.bm = 256; d.dma = 1; }
+      long long t256 = 0;
+      for (int p = 0; p < d.nphase; ++p) t256 += ic_cdiv((long long)d.N * d.ph[p].Hg * d.ph[p].Wg, 256);
+      // as ig_kernel_x3d: K split only for one-phase maps (a transposed conv's phases have unequal taps)
+      if (t256 >= 256 || (d.nphase == 1 && t256 >= IG_X3D_MINT)) { d.bm = 256; d.dma = 1; }
     }
   }
   else if (d.Cout >= 64) { d.bm = 128; d.bn = 64; }
@@ -1255,8 +1257,8 @@ int ig_run(IgDesc& d, hipStream_t s) {
     for (int p = 0; p < d.nphase; ++p) mt = mt > d.ph[p].mtiles ? mt : d.ph[p].mtiles;
     if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
     if (d.bf16) {
-      if (!d.xb || d.nphase != 1 || d.Cin % 64 != 0) return IC_ERR_ARG;
-      hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.ksplit), dim3(512), 0, s, d);
+      if (!d.xb || d.Cin % 64 != 0) return IC_ERR_ARG;
+      hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     } else {
       hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     }

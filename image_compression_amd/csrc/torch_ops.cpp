@@ -373,6 +373,43 @@ Tensor conv_transpose2d_dgrad_xb(const Tensor& dy, const Tensor& dyb, const Tens
   return dx;
 }
 
+Tensor conv2d_dgrad_xb(const Tensor& dy, const Tensor& dyb, const Tensor& w, const Tensor& x, int64_t stride,
+                       int64_t pad, int64_t math) {
+  check_operand(dy, "dy");
+  check_operand(w, "weight");
+  check_copy(dyb, dy, "dyb");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dx = new_act(dy, x.size(0), x.size(1), x.size(2), x.size(3));
+  const ic_act ag = act_of(dy), adx = act_of(dx);
+  const int k = (int)w.size(2);
+  const size_t nb = ic_conv2d_dgrad_ws_ex(&ag, k, (int)stride, (int)pad, &adx, (int)math | IC_MATH_XB);
+  Tensor ws = workspace(dy, nb);
+  check_rc(ic_conv2d_dgrad_xb(&ag, dyb.data_ptr(), w.data_ptr<float>(), k, (int)stride, (int)pad, &adx, (int)math,
+                              ws.data_ptr(), nb, stream_of(dy)),
+           "conv2d_dgrad_xb");
+  return dx;
+}
+Tensor conv_transpose2d_fwd_xb(const Tensor& x, const Tensor& xb, const Tensor& w, const c10::optional<Tensor>& b,
+                               int64_t stride, int64_t pad, int64_t opad, int64_t act, int64_t math) {
+  check_operand(x, "x");
+  check_operand(w, "weight");
+  check_copy(xb, x, "xb");
+  if (b.has_value()) check_operand(*b, "bias");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == x.size(1) && w.size(2) == w.size(3), "conv_transpose2d: weight ", w.sizes(),
+              " does not match input ", x.sizes());
+  const int64_t k = w.size(2);
+  const int64_t ho = (x.size(2) - 1) * stride - 2 * pad + k + opad, wo = (x.size(3) - 1) * stride - 2 * pad + k + opad;
+  Tensor y = new_act(x, x.size(0), w.size(1), ho, wo);
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb = ic_conv_transpose2d_fwd_ws_ex(&ax, (int)k, (int)stride, (int)pad, &ay, (int)math | IC_MATH_XB);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_conv_transpose2d_fwd_xb(&ax, xb.data_ptr(), w.data_ptr<float>(), opt_ptr(b), (int)k, (int)stride,
+                                      (int)pad, &ay, (int)act, (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "conv_transpose2d_fwd_xb");
+  return y;
+}
+
 // ---------------------------------------------------------------- elementwise, losses, entropy models
 // Reference interfaces: NonNegativeParam.forward (layers/gdn.py:59-62), Lower/UpperBound
 // (layers/bound.py:28-59), ReLU / torch.abs (prior_analysis.py:65, bmshl2018.py:72), the exp-clamp of
@@ -889,6 +926,15 @@ Tensor conv_transpose2d_dgrad_xb_meta(const Tensor& dy, const Tensor&, const Ten
   return conv_transpose2d_dgrad_meta(dy, w, x, s, p, m);
 }
 
+Tensor conv2d_dgrad_xb_meta(const Tensor& dy, const Tensor&, const Tensor& w, const Tensor& x, int64_t s, int64_t p,
+                            int64_t m) {
+  return conv2d_dgrad_meta(dy, w, x, s, p, m);
+}
+Tensor conv_transpose2d_fwd_xb_meta(const Tensor& x, const Tensor&, const Tensor& w, const c10::optional<Tensor>& b,
+                                    int64_t stride, int64_t pad, int64_t op, int64_t act, int64_t math) {
+  return conv_transpose2d_fwd_meta(x, w, b, stride, pad, op, act, math);
+}
+
 // elementwise / loss / entropy shape kernels
 Tensor like_meta1(const Tensor& x) { return at::empty_like(x, at::MemoryFormat::Preserve); }
 Tensor nonneg_fwd_meta(const Tensor& p, double, double) { return like_meta1(p); }
@@ -994,6 +1040,9 @@ TORCH_LIBRARY(imgcomp, m) {
         "int math) -> Tensor");
   m.def("conv_transpose2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, "
         "int math) -> Tensor");
+  m.def("conv2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, int math) -> Tensor");
+  m.def("conv_transpose2d_fwd_xb(Tensor x, Tensor xb, Tensor weight, Tensor? bias, int stride, int padding, "
+        "int output_padding, int act, int math) -> Tensor");
   m.def("nonneg_fwd(Tensor p, float bound, float pedestal) -> Tensor");
   m.def("nonneg_bwd(Tensor p, Tensor grad, float bound) -> Tensor");
   m.def("nonneg_multi_fwd(Tensor[] p, float[] bound, float[] pedestal) -> Tensor[]");
@@ -1048,6 +1097,8 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb);
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb);
+  m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb);
+  m.impl("conv_transpose2d_fwd_xb", conv_transpose2d_fwd_xb);
   m.impl("nonneg_fwd", nonneg_fwd);
   m.impl("nonneg_bwd", nonneg_bwd);
   m.impl("nonneg_multi_fwd", nonneg_multi_fwd);
@@ -1094,6 +1145,8 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb_meta);
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb_meta);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb_meta);
+  m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb_meta);
+  m.impl("conv_transpose2d_fwd_xb", conv_transpose2d_fwd_xb_meta);
   m.impl("nonneg_fwd", nonneg_fwd_meta);
   m.impl("nonneg_bwd", nonneg_bwd_meta);
   m.impl("nonneg_multi_fwd", nonneg_multi_fwd_meta);

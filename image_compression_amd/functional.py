@@ -177,13 +177,17 @@ class Conv2dFn(Function):
         stride, padding, act, has_b, math = ctx.conf
         # the bias gradient formed by gy's producer (taken only where this node owns the bias gradient)
         pre = _take_colsum(gy) if (has_b and not act and ctx.needs_input_grad[2]) else None
+        gyb = _take_bf16(gy) if (math & MATH["bf16"]) and not act else None
         if act:
             gy = relu_bwd(y, gy)
         gy = _cl(gy)
         dx = dw = db = None
         ops, k = _lib.ops(), w.shape[2]
         if ctx.needs_input_grad[0]:
-            dx = ops.conv2d_dgrad(gy, w, x, stride, padding, math)
+            if gyb is not None and gyb.stride() == gy.stride():
+                dx = ops.conv2d_dgrad_xb(gy, gyb, w, x, stride, padding, math)
+            else:
+                dx = ops.conv2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
             dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
@@ -203,7 +207,11 @@ class ConvTranspose2dFn(Function):
         b = None if bias is None else bias.contiguous()
         if w.shape[0] != x.shape[1] or w.shape[2] != w.shape[3]:
             raise RuntimeError(f"conv_transpose2d: weight {tuple(w.shape)} does not match input {tuple(x.shape)}")
-        y = _lib.ops().conv_transpose2d_fwd(x, w, b, stride, padding, output_padding, int(act), int(math))
+        xb = _take_bf16(x) if int(math) & MATH["bf16"] else None
+        if xb is not None:
+            y = _lib.ops().conv_transpose2d_fwd_xb(x, xb, w, b, stride, padding, output_padding, int(act), int(math))
+        else:
+            y = _lib.ops().conv_transpose2d_fwd(x, w, b, stride, padding, output_padding, int(act), int(math))
         _log_plan("conv_transpose2d_fwd", x, y, w.shape[2], stride, padding, math)
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
@@ -221,11 +229,11 @@ class ConvTranspose2dFn(Function):
         gy = _cl(gy)
         dx = dw = db = None
         ops, k = _lib.ops(), w.shape[2]
-        if ctx.needs_input_grad[0] and gyb is not None and gyb.stride() == gy.stride():
-            dx = ops.conv_transpose2d_dgrad_xb(gy, gyb, w, x, stride, padding, math)
-            _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
-        elif ctx.needs_input_grad[0]:
-            dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
+        if ctx.needs_input_grad[0]:
+            if gyb is not None and gyb.stride() == gy.stride():
+                dx = ops.conv_transpose2d_dgrad_xb(gy, gyb, w, x, stride, padding, math)
+            else:
+                dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
             dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)

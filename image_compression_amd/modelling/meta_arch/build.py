@@ -62,9 +62,10 @@ def set_compute_dtype(model, dtype):
             for m in sub.modules():
                 if isinstance(m, (Conv2d, ConvTranspose2d)):
                     m.math = flag
-    # bf16 (C3): a GDN feeding a 192 -> 192 conv forward writes its output's bf16 copy, and one
-    # behind a 192-input transposed conv its input gradient's, for those convs' bf16 DMA tiles
-    # (csrc/igemm.hip ig_kernel_b16d: Cout 192, Cin % 64 == 0, one phase)
+    # bf16 (C3): a GDN feeding a 192-output conv / transposed conv writes its output's bf16 copy for
+    # that conv's forward, and one behind a 192-input conv / transposed conv its input gradient's for
+    # that conv's input gradient, both on the bf16 DMA tiles (csrc/igemm.hip ig_kernel_b16d: Cout 192,
+    # Cin % 64 == 0; a copy the plan does not use is ignored)
     for m in model.modules():
         if isinstance(m, GDN):
             m.xb = 0
@@ -79,9 +80,13 @@ def set_compute_dtype(model, dtype):
                     continue
                 nxt = mods[i + 1] if i + 1 < len(mods) else None
                 prv = mods[i - 1] if i > 0 else None
-                if (isinstance(nxt, Conv2d) and not isinstance(nxt, ConvTranspose2d) and nxt.out_channels == 192
-                        and nxt.in_channels % 64 == 0):
+                # the next conv's forward / the previous conv's input gradient: out 192, in % 64 == 0
+                if isinstance(nxt, Conv2d) and nxt.out_channels == 192 and nxt.in_channels % 64 == 0:
+                    m.xb |= 1
+                if isinstance(nxt, ConvTranspose2d) and nxt.out_channels == 192 and nxt.in_channels % 64 == 0:
                     m.xb |= 1
                 if isinstance(prv, ConvTranspose2d) and prv.in_channels == 192 and prv.out_channels % 64 == 0:
+                    m.xb |= 2
+                if isinstance(prv, Conv2d) and prv.in_channels == 192 and prv.out_channels % 64 == 0:
                     m.xb |= 2
     return model

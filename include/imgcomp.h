@@ -102,9 +102,9 @@ int ic_conv_transpose2d_wgrad(const ic_act* x, const ic_act* dy, int k, int stri
  *      (the im2col fallback, the row-stationary transposed edge) ignore it.  The caller owns the invalidation: any change of
  *      the weight needs a forward without the flag first. */
 #define IC_MATH_WPACKED 4
-/*      IC_MATH_XB (or-ed into IC_MATH_BF16, in the workspace query of a conv forward / transposed-conv
- *      input gradient whose caller passes the input's bf16 copy to ic_conv2d_fwd_xb /
- *      ic_conv_transpose2d_dgrad_xb): the workspace leaves out the space the conversion of x would take. */
+/*      IC_MATH_XB (or-ed into IC_MATH_BF16, in the workspace query of a conv / transposed conv forward or
+ *      input gradient whose caller passes the input's bf16 copy to the matching *_xb entry point): the
+ *      workspace leaves out the space the conversion of x would take. */
 #define IC_MATH_XB 8
 size_t ic_conv2d_fwd_ws_ex(const ic_act* x, int k, int stride, int pad, const ic_act* y, int math);
 int ic_conv2d_fwd_ex(const ic_act* x, const float* w, const float* b, int k, int stride, int pad,
@@ -177,6 +177,12 @@ int ic_conv2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const floa
                      const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
 int ic_conv_transpose2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
                                  const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
+/* the same for the phases of a transposed conv forward / conv input gradient (stride-2 sub-pixel phases on
+ * the DMA tiles where every phase has >= 256 tiles of 256 rows) */
+int ic_conv_transpose2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const float* b, int k, int stride,
+                               int pad, const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
+int ic_conv2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
+                       const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- launch-plan query: which kernel instance, tile and K / pixel split a conv or GDN op would launch
  *      for these shapes (no launch, no device access; the same decision code as the launching entry

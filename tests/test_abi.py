@@ -172,9 +172,12 @@ def test_plan_query_c2_instances():
     assert p["kernel"] == "ig_fp32"
     p = _lib.plan("conv2d_fwd", x, y, 5, 2, 2, 1)
     assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_bf16_dma", 256, 1)
-    # bf16 operands: a transposed conv's phases stay on ig_kernel_bf16 (the DMA tiles are one-phase)
+    # bf16 operands: a transposed conv's four phases on the DMA tiles too (each >= 256 tiles) ...
     p = _lib.plan("conv2d_dgrad", y, x, 5, 2, 2, 1)
-    assert (p["kernel"], p["bm"]) == ("ig_bf16", 128)
+    assert (p["kernel"], p["bm"], p["ksplit"]) == ("ig_bf16_dma", 256, 1)
+    # ... but not below 256 tiles (no K split across unequal phases)
+    p = _lib.plan("conv_transpose2d_fwd", _act(8, 192, 32, 32), _act(8, 192, 64, 64), 5, 2, 2, 1)
+    assert (p["kernel"], p["bm"]) == ("ig_split_bf16", 64)
     p = _lib.plan("conv_transpose2d_dgrad", x, y, 5, 2, 2, 1)
     assert (p["kernel"], p["bm"]) == ("ig_bf16_dma", 256)
     # small maps: 64-row tiles with split-K
@@ -321,6 +324,12 @@ def _meta_cases():
                            [s, (192, 192), (192,), (192,), s]),
         "conv2d_fwd_xb": (lambda o: o.conv2d_fwd_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5),
                                                     None, 2, 2, 0, 3), [(2, 192, 8, 8)]),
+        "conv2d_dgrad_xb": (lambda o: o.conv2d_dgrad_xb(_meta(2, 192, 8, 8, cl=True),
+                                                        _meta(2, 192, 8, 8, cl=True, dtype=torch.bfloat16),
+                                                        _meta(192, 192, 5, 5), x, 2, 2, 3), [s]),
+        "conv_transpose2d_fwd_xb": (lambda o: o.conv_transpose2d_fwd_xb(
+            _meta(2, 192, 8, 8, cl=True), _meta(2, 192, 8, 8, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5),
+            None, 2, 2, 1, 0, 3), [s]),
         "conv_transpose2d_dgrad_xb": (lambda o: o.conv_transpose2d_dgrad_xb(
             x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5), _meta(2, 192, 8, 8, cl=True), 2, 2, 3),
                                       [(2, 192, 8, 8)]),

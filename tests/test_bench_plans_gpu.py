@@ -54,8 +54,10 @@ def test_c2_conv_layer(math):
     pf = _lib.plan("conv2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
-    # bf16 operands: the one-phase forward on the DMA tiles (ig_kernel_b16d), the four-phase dgrad not
-    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == ((kern, bm, 1) if math == 2 else ("ig_bf16_dma", 256, 1)), pf
+    # bf16 operands: the forward and the four-phase dgrad on the DMA tiles (ig_kernel_b16d)
+    if math == 1:
+        kern, bm = "ig_bf16_dma", 256
+    assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, bm, 1), pf
     assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, bm, 1), pd
     # weight gradients: split arithmetic, or bf16 operands on the same two-wave kernel
     assert (pw["kernel"], pw["variant"]) == ("wg_split" if math == 2 else "wg_bf16", 1), pw
@@ -92,9 +94,11 @@ def test_c2_tconv_layer(math):
     pf = _lib.plan("conv_transpose2d_fwd", xd.detach(), y.detach(), 5, 2, 2, math)
     pd = _lib.plan("conv_transpose2d_dgrad", gy, xd.detach(), 5, 2, 2, math)
     pw = _lib.plan("conv_transpose2d_wgrad", xd.detach(), gy, 5, 2, 2, math)
+    # bf16 operands: the four-phase forward and the one-phase dgrad on the DMA tiles (ig_kernel_b16d)
+    if math == 1:
+        kern, bm = "ig_bf16_dma", 256
     assert (pf["kernel"], pf["bm"], pf["ksplit"]) == (kern, bm, 1), pf
-    # bf16 operands: the one-phase dgrad on the DMA tiles (ig_kernel_b16d)
-    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == ((kern, bm, 1) if math == 2 else ("ig_bf16_dma", 256, 1)), pd
+    assert (pd["kernel"], pd["bm"], pd["ksplit"]) == (kern, bm, 1), pd
     assert pw["kernel"] == ("wg_split" if math == 2 else "wg_bf16"), pw
     xr = x.double().requires_grad_(True)
     wr = w.double().requires_grad_(True)
