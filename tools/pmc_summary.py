@@ -43,7 +43,10 @@ def main(src, dst):
         "fetch_bytes_corrected": 2.0 * f_kib * 1024.0,
         "write_bytes": w_kib * 1024.0,
         "traffic_bytes_per_launch": 2.0 * f_kib * 1024.0 + w_kib * 1024.0,
-        "algorithmic_bytes_per_launch": 4.0 * (32 * 192 * 128 * 128 + 192 * 192 * 25 + 32 * 192 * 64 * 64),
+        # bf16 DMA tiles (C3): the input's bf16 copy and the bf16 weight plane, fp32 output
+        "algorithmic_bytes_per_launch": ((2.0 * (32 * 192 * 128 * 128 + 192 * 192 * 25) + 4.0 * 32 * 192 * 64 * 64)
+                                         if "b16d" in KERNEL else
+                                         4.0 * (32 * 192 * 128 * 128 + 192 * 192 * 25 + 32 * 192 * 64 * 64)),
         "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KiB -> bytes",
     }
     os.makedirs(os.path.dirname(dst), exist_ok=True)
