@@ -151,7 +151,8 @@ def dominant_kernel_roofline(dev, reps=20, live_ms=None, live_launches=0, math="
             "peak_note": {"fp32_split": "algorithmic fp32 FLOP/s; peak = bf16 dense MFMA 2500 TF / 6 products per fp32 MAC",
                           "bf16": "algorithmic FLOP/s; peak = bf16 dense MFMA spec (2500 TF)"}.get(math, "fp32 dense MFMA spec"),
             "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "kernel": kern + (" + weight pack + input bf16 conversion" if math == "bf16" else " + weight pack") +
+            "kernel": kern + (" + weight pack (live: the input's bf16 copy comes from the GDN before it; the isolated "
+                              "loop converts x itself)" if math == "bf16" else " + weight pack") +
                       ": conv2d 5x5 s2 192->192 @ 32x128x128 (g_a layer 2 fwd)",
             "flop_per_launch": flop, "ms_per_launch": round(ms, 4),
             "timing": (f"live: HIP events on the launch stream around the layer's {live_launches} launches "
