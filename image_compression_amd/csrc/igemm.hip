@@ -942,6 +942,9 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
 #ifndef IG_B16D
 #define IG_B16D 1
 #endif
+#ifndef IG_B16D_DMA_J
+#define IG_B16D_DMA_J 4  // the next chunk's DMA issues before column tile j's MFMAs (as ig_kernel_x3d)
+#endif
 __device__ __forceinline__ int ig_swb(int r) { return (r >> 1) & 7; }
 
 __global__ void __launch_bounds__(512, 1) ig_kernel_b16d(const IgDesc d) {
@@ -1046,7 +1049,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_b16d(const IgDesc d) {
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      if (j == IG_X3D_DMA_J && c + 1 < ce) {
+      if (j == IG_B16D_DMA_J && c + 1 < ce) {
         issue(cn, tn, (c + 1 - cb) & 1);
         if (++tn == T) { tn = 0; ++cn; }
       }
