@@ -63,6 +63,9 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef X3W_STAMP
 #define X3W_STAMP 0  // diagnostic: per-iteration s_memtime stamps of gdn_bwd_x3w_kernel into the workspace
 #endif
+#ifndef GDN_BWD_X3W_BF16
+#define GDN_BWD_X3W_BF16 0  // 1: C3's GDN backward (bf16 operands) on gdn_bwd_x3w_kernel<192, INV, 1> (r07u: 0.341 vs 0.333 ms at 128^2, C3 -1 %); 0: gdn_bwd_fused_kernel
+#endif
 #ifndef X3W_SGB
 #define X3W_SGB 1  // gdn_bwd_x3w_kernel: interleave phase A / epilogue with the MFMAs (sched_group_barrier)
 #endif
@@ -884,18 +887,23 @@ __global__ void __launch_bounds__(512, 2)
 // rows past P load row P-1 with q = dv = 0, and their dx goes to a dump slot (no branches around
 // memory operations, so the compiler's waitcnt pass never waits for the stores).
 // dbeta and the dx column sums (the producing conv's bias gradient) accumulate in per-lane LDS slots.
-template <int C, bool INV>
+// NP = 1 (IC_MATH_BF16, config C3, round 5): the same kernel on bf16 operands -- gamma, q and x^2
+// rounded to nearest even, one plane each, one product per MFMA step; XB: dx also as a compact bf16
+// copy (dxb) for the previous transposed conv's input gradient (ig_kernel_b16d).
+template <int C, bool INV, int NP = 3, bool XB = false>
 __global__ void __launch_bounds__(256, 1)
     gdn_bwd_x3w_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
                        const float* __restrict__ gamma, float* __restrict__ dx,
-                       float* __restrict__ slab, uint32_t P) {
+                       float* __restrict__ slab, uint32_t P, __bf16* __restrict__ dxb = nullptr) {
   static_assert(C == 192, "4 waves x 48 dx columns, 2 x 2 dgamma quadrants of 96");
+  static_assert(NP == 3 || NP == 1, "split (3 planes) or bf16 (1 plane)");
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   constexpr int BM = 16, NT = 256, K32 = C / 32;
-  constexpr int PL = BM * C;      // bf16 elements per plane
-  constexpr int PSET = 6 * PL;    // q planes then x^2 planes
-  __shared__ __attribute__((aligned(16))) __bf16 pls[2 * PSET];      // 72 KB: two plane sets
+  constexpr int PL = BM * C;        // bf16 elements per plane
+  constexpr int PSET = 2 * NP * PL; // q planes then x^2 planes
+  __shared__ __attribute__((aligned(16))) __bf16 pls[2 * PSET];      // 72 KB (NP 3): two plane sets
   __shared__ __attribute__((aligned(16))) floatx4v xdv[2][6][NT];     // 48 KB: x (j) and dv (3 + j) per lane
   __shared__ __attribute__((aligned(16))) floatx4v acc_s[6][NT];      // 24 KB: dbeta (j), dx column sums (3 + j)
 
@@ -907,23 +915,28 @@ __global__ void __launch_bounds__(256, 1)
   if (tile >= ntiles) return;  // whole block: before any barrier
 
   // gamma^T fragments: gx[p][j][s] = plane p of gamma[n = 32s + 8lg + e][k = 48w + 16j + li]
-  b8 gx[3][3][K32];
+  b8 gx[NP][3][K32];
 #pragma unroll
   for (int j = 0; j < 3; ++j)
 #pragma unroll
     for (int s = 0; s < K32; ++s)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        __bf16 hh, mm, ll;
-        split3_bf16(gamma[(size_t)(32 * s + 8 * lg + e) * C + 48 * w + 16 * j + li], hh, mm, ll);
-        gx[0][j][s][e] = hh;
-        gx[1][j][s][e] = mm;
-        gx[2][j][s][e] = ll;
+        const float gv = gamma[(size_t)(32 * s + 8 * lg + e) * C + 48 * w + 16 * j + li];
+        if constexpr (NP == 1) {
+          gx[0][j][s][e] = (__bf16)gv;  // round to nearest even
+        } else {
+          __bf16 hh, mm, ll;
+          split3_bf16(gv, hh, mm, ll);
+          gx[0][j][s][e] = hh;
+          gx[NP - 2][j][s][e] = mm;
+          gx[NP - 1][j][s][e] = ll;
+        }
       }
   // the 216 gamma registers live in AGPRs (MFMA A operands may be AGPRs): the 256 arch VGPRs of the
   // wave then hold the dgamma accumulators, the landing registers and phase A
 #pragma unroll
-  for (int p = 0; p < 3; ++p)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -950,6 +963,18 @@ __global__ void __launch_bounds__(256, 1)
     ln[j] = *(const floatx4v*)(norm + o);
     ld[j] = *(const floatx4v*)(dy + o);
   };
+  // a float4 into NP planes at dst (plane stride PL): the exact split, or rounded to nearest even
+  auto put_planes = [&](__bf16* dst, floatx4v v) {
+    if constexpr (NP == 1) {
+      *(b4*)dst = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
+    } else {
+      b4 h, m, l;
+      split3_bf16x4(v, h, m, l);
+      *(b4*)dst = h;
+      *(b4*)(dst + PL) = m;
+      *(b4*)(dst + 2 * PL) = l;
+    }
+  };
   // phase A, element group j of tile t from the landing registers into buffer b
   auto phase_a = [&](uint32_t t, int b, int j) {
     // rows past P (and a tile past the end) contribute nothing: q = dv = 0 by selects (no branch)
@@ -965,15 +990,8 @@ __global__ void __launch_bounds__(256, 1)
       dv[e] = valid ? d : 0.f;
     }
     __bf16* sp = pls + b * PSET + pl_off<C>(li, cbase + 16 * j);
-    b4 h, m, l;
-    split3_bf16x4(qv, h, m, l);
-    *(b4*)sp = h;
-    *(b4*)(sp + PL) = m;
-    *(b4*)(sp + 2 * PL) = l;
-    split3_bf16x4(xv * xv, h, m, l);
-    *(b4*)(sp + 3 * PL) = h;
-    *(b4*)(sp + 4 * PL) = m;
-    *(b4*)(sp + 5 * PL) = l;
+    put_planes(sp, qv);
+    put_planes(sp + NP * PL, xv * xv);
     xdv[b][j][tid] = xv;
     xdv[b][3 + j][tid] = dv;
     acc_s[j][tid] += qv;
@@ -1030,14 +1048,13 @@ __global__ void __launch_bounds__(256, 1)
     floatx4v acc[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    auto qfrag = [&](int st, b8 (&f)[3]) {
+    auto qfrag = [&](int st, b8 (&f)[NP]) {
       const int off = pl_off<C>(li, 32 * st + 8 * lg);
-      f[0] = *(const b8*)(sp + off);
-      f[1] = *(const b8*)(sp + PL + off);
-      f[2] = *(const b8*)(sp + 2 * PL + off);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) f[p] = *(const b8*)(sp + p * PL + off);
     };
-    b8 fa[3], fb[3];
-    b8 av[3][3], bb[2][3];  // dgamma GEMM fragments (read during the dx GEMM's last K step)
+    b8 fa[NP], fb[NP];
+    b8 av[3][NP], bb[2][NP];  // dgamma GEMM fragments (read during the dx GEMM's last K step)
     qfrag(0, fa);
     // phase A(t+G) part pr in six slices, one between each (K step, column tile) group of six MFMAs
     floatx4v pq, pd, pxv;
@@ -1057,17 +1074,9 @@ __global__ void __launch_bounds__(256, 1)
           pd[e] = valid ? d : 0.f;
         }
       } else if (k == 2) {  // q's split planes
-        b4 h, m, l;
-        split3_bf16x4(pq, h, m, l);
-        *(b4*)pp = h;
-        *(b4*)(pp + PL) = m;
-        *(b4*)(pp + 2 * PL) = l;
+        put_planes(pp, pq);
       } else if (k == 3) {  // x^2's split planes
-        b4 h, m, l;
-        split3_bf16x4(pxv * pxv, h, m, l);
-        *(b4*)(pp + 3 * PL) = h;
-        *(b4*)(pp + 4 * PL) = m;
-        *(b4*)(pp + 5 * PL) = l;
+        put_planes(pp + NP * PL, pxv * pxv);
       } else if (k == 4) {
         xdv[cb ^ 1][pr][tid] = pxv;
         xdv[cb ^ 1][3 + pr][tid] = pd;
@@ -1082,12 +1091,14 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int st = 2 * pr + h2;
-        b8 (&cur)[3] = h2 ? fb : fa;
-        b8 (&nxt)[3] = h2 ? fa : fb;
+        b8 (&cur)[NP] = h2 ? fb : fa;
+        b8 (&nxt)[NP] = h2 ? fa : fb;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           if (j == 0 && st + 1 < K32) qfrag(st + 1, nxt);
-          if (!(X3W_ABL & 8)) {
+          if constexpr (NP == 1) {
+            if (!(X3W_ABL & 8)) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[0], acc[j], 0, 0, 0);
+          } else if (!(X3W_ABL & 8)) {
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[2], acc[j], 0, 0, 0);
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][st], cur[1], acc[j], 0, 0, 0);
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[2][j][st], cur[0], acc[j], 0, 0, 0);
@@ -1098,9 +1109,9 @@ __global__ void __launch_bounds__(256, 1)
           pa_slice(pr, 3 * h2 + j);
           if (X3W_SGB) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
+            for (int k = 0; k < (NP == 1 ? 1 : 6); ++k) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+              __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 24 : 4, 0);  // VALU
             }
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -1113,24 +1124,29 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) av[i][p] = tr8(sp + p * PL, 96 * wm2 + 32 * i);
+      for (int p = 0; p < NP; ++p) av[i][p] = tr8(sp + p * PL, 96 * wm2 + 32 * i);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) bb[0][p] = tr8(sp + (3 + p) * PL, 96 * wn2);
+    for (int p = 0; p < NP; ++p) bb[0][p] = tr8(sp + (NP + p) * PL, 96 * wn2);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       if (j + 1 < 3)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bb[(j + 1) & 1][p] = tr8(sp + (3 + p) * PL, 96 * wn2 + 32 * (j + 1));
-      const b8 (&bc)[3] = bb[j & 1];
+        for (int p = 0; p < NP; ++p) bb[(j + 1) & 1][p] = tr8(sp + (NP + p) * PL, 96 * wn2 + 32 * (j + 1));
+      const b8 (&bc)[NP] = bb[j & 1];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         if (X3W_ABL & 4) continue;
+        if constexpr (NP == 1) {
+          dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[0], dg[i][j], 0, 0, 0);
+          continue;
+        } else {
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][2], bc[0], dg[i][j], 0, 0, 0);
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bc[1], dg[i][j], 0, 0, 0);
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[2], dg[i][j], 0, 0, 0);
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][1], bc[0], dg[i][j], 0, 0, 0);
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[1], dg[i][j], 0, 0, 0);
         dg[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i][0], bc[0], dg[i][j], 0, 0, 0);
+        }
       }
       {  // epilogue, element group j
         const uint32_t m = tile * BM + li;
@@ -1138,14 +1154,18 @@ __global__ void __launch_bounds__(256, 1)
         const floatx4v xv = xdv[cb][j][tid], dv = xdv[cb][3 + j][tid];
         const floatx4v d = dv + 2.f * xv * acc[j];
         if (!(X3W_ABL & 16)) *(floatx4v*)dst = d;
+        if constexpr (XB) {  // the bf16 copy; rows past P to the (16-B) dump slot's first 8 B
+          __bf16* db = m < P ? dxb + (size_t)m * C + cbase + 16 * j : (__bf16*)(dump + tid * 4);
+          *(b4*)db = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(d[0], d[1]), ic_cvt_pk_bf16(d[2], d[3])});
+        }
         acc_s[3 + j][tid] += d;
       }
       if (X3W_SGB) {
 #pragma unroll
-        for (int k = 0; k < 18; ++k) {
+        for (int k = 0; k < (NP == 1 ? 3 : 18); ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          if (k < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (the next bb)
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+          if (k < 6) __builtin_amdgcn_sched_group_barrier(0x100, NP == 1 ? 2 : 1, 0);  // DS read (the next bb)
+          __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : 2, 0);  // VALU
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1301,6 +1321,28 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum,
                   void* dxb) {
   float* slab = (float*)ws;
+  if (split == 2 && C == 192 && GDN_BWD_X3W_BF16) {  // bf16 operands (C3) on the pipelined one-wave kernel
+    const int grid = bwd_grid(P);
+    if (grid < 1) return IC_OK;
+    __bf16* b = (__bf16*)dxb;
+    if (inverse && dxb)
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, true, 1, true>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma,
+                         dx, slab, (uint32_t)P, b);
+    else if (inverse)
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, true, 1>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx,
+                         slab, (uint32_t)P, b);
+    else if (dxb)
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, false, 1, true>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma,
+                         dx, slab, (uint32_t)P, b);
+    else
+      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, false, 1>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx,
+                         slab, (uint32_t)P, b);
+    IC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((GDN_SLAB(192) + 63) / 64), dim3(256), 0, s, slab, grid, 192,
+                       dgamma, dbeta, dxsum);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
   if (split == 2 && C == 192 && dxb)
     return gdn_bwd_fused_launch<192, true, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab,
                                                        s, dxb);
