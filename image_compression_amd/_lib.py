@@ -116,6 +116,10 @@ SIGNATURES = {
     "ic_conv_transpose2d_dgrad_xb": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size,
                                              c_void]),
     "ic_conv2d_dgrad_xb": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size, c_void]),
+    "ic_conv2d_wgrad_xb": (c_int, [_ACT, c_void, _ACT, c_void, c_int, c_int, c_int, c_void, c_void, c_int, c_void,
+                                   c_size, c_void]),
+    "ic_conv_transpose2d_wgrad_xb": (c_int, [_ACT, c_void, _ACT, c_void, c_int, c_int, c_int, c_void, c_void, c_int,
+                                             c_void, c_size, c_void]),
     "ic_conv_transpose2d_fwd_xb": (c_int, [_ACT, c_void, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int,
                                            c_void, c_size, c_void]),
     "ic_nonneg_fwd": (c_int, [c_void, c_ll, c_float, c_float, c_void, c_void]),

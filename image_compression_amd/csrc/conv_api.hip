@@ -392,8 +392,10 @@ int transposed_impl(const ic_act* x, const float* W, const float* bias, int k, i
 }
 
 // dW[g][c][ky][kx] = sum_p G[p][g] * X[p*s + ky - pad][c]; db = colsum(bias_src)
+// g16 / x16: G's and X's bf16 copies (ic_conv*_wgrad_xb; used by the bf16 tap-group kernel, else ignored)
 int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, float* dw,
-               const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0) {
+               const ic_act* bias_src, float* db, void* ws, size_t wsb, hipStream_t s, size_t* need, int math = 0,
+               const void* g16 = nullptr, const void* x16 = nullptr) {
   if (k < 1 || k * k > IC_MAXT || stride < 1) return IC_ERR_ARG;
   if (G->n != X->n) return IC_ERR_ARG;
   if (!act_fits32(G) || !act_fits32(X)) return IC_ERR_ARG;  // 32-bit element offsets in the kernels
@@ -409,6 +411,7 @@ int wgrad_impl(const ic_act* G, const ic_act* X, int k, int stride, int pad, flo
   d.split_ok = (math & IC_MATH_SPLIT) ? 1 : 0;
   d.bf16 = (math & IC_MATH_BF16) ? 1 : 0;
   d.x3 = (d.split_ok || d.bf16) ? 1 : 0;  // the bf16 form runs on the split kernel family
+  if (d.bf16) { d.g16 = g16; d.x16 = x16; }
   int kk_of_t[IC_MAXT];
   for (int t = 0; t < d.T; ++t) {
     d.dy[t] = t / k - pad; d.dx[t] = t % k - pad; kk_of_t[t] = t;
@@ -651,6 +654,10 @@ int ic_conv2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int
                        void* ws, size_t ws_bytes, void* stream) {
   return wgrad_impl(dy, x, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
 }
+int ic_conv2d_wgrad_xb(const ic_act* x, const void* xb, const ic_act* dy, const void* dyb, int k, int stride, int pad,
+                       float* dw, float* db, int math, void* ws, size_t ws_bytes, void* stream) {
+  return wgrad_impl(dy, x, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math, dyb, xb);
+}
 
 size_t ic_conv_transpose2d_wgrad_ws(const ic_act* x, const ic_act* dy, int k, int stride, int pad) {
   size_t n = 0;
@@ -670,6 +677,11 @@ size_t ic_conv_transpose2d_wgrad_ws_ex(const ic_act* x, const ic_act* dy, int k,
 int ic_conv_transpose2d_wgrad_ex(const ic_act* x, const ic_act* dy, int k, int stride, int pad, float* dw, float* db,
                                  int math, void* ws, size_t ws_bytes, void* stream) {
   return wgrad_impl(x, dy, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math);
+}
+int ic_conv_transpose2d_wgrad_xb(const ic_act* x, const void* xb, const ic_act* dy, const void* dyb, int k,
+                                 int stride, int pad, float* dw, float* db, int math, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  return wgrad_impl(x, dy, k, stride, pad, dw, dy, db, ws, ws_bytes, (hipStream_t)stream, nullptr, math, xb, dyb);
 }
 
 }  // extern "C"

@@ -98,6 +98,8 @@ struct WgDesc {
   int bf16;        // with x3: bf16 operands on the two-wave kernel (wg_x3d_kernel<..., 1>); cleared by wg_plan
                    // where that kernel does not run
   int split_ok;    // split arithmetic allowed (IC_MATH_SPLIT): wg_plan's fallback when bf16 is cleared
+  const void* g16; // with bf16: G and X as bf16 copies (compact NHWC, the fp32 tensors' element offsets),
+  const void* x16; //   read by the producer waves of wg_x3p_kernel instead of converting (C3, round 5)
   int dy[IC_MAXT], dx[IC_MAXT];
 };
 

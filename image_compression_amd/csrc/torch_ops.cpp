@@ -410,6 +410,40 @@ Tensor conv_transpose2d_fwd_xb(const Tensor& x, const Tensor& xb, const Tensor& 
   return y;
 }
 
+template <bool TR>
+std::tuple<Tensor, Tensor> wgrad_xb(const Tensor& x, const Tensor& xb, const Tensor& dy, const Tensor& dyb,
+                                    const Tensor& w, int64_t stride, int64_t pad, bool bias, int64_t math) {
+  check_operand(x, "x");
+  check_operand(dy, "dy");
+  check_copy(xb, x, "xb");
+  check_copy(dyb, dy, "dyb");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dw = at::empty_like(w, at::MemoryFormat::Contiguous);
+  Tensor db = at::empty({bias ? (TR ? w.size(1) : w.size(0)) : 0}, w.options());
+  const ic_act ax = act_of(x), ag = act_of(dy);
+  const int k = (int)w.size(2);
+  const size_t nb = TR ? ic_conv_transpose2d_wgrad_ws_ex(&ax, &ag, k, (int)stride, (int)pad, (int)math)
+                       : ic_conv2d_wgrad_ws_ex(&ax, &ag, k, (int)stride, (int)pad, (int)math);
+  Tensor ws = workspace(dy, nb);
+  float* dbp = bias ? db.data_ptr<float>() : nullptr;
+  const int rc = TR ? ic_conv_transpose2d_wgrad_xb(&ax, xb.data_ptr(), &ag, dyb.data_ptr(), k, (int)stride, (int)pad,
+                                                   dw.data_ptr<float>(), dbp, (int)math, ws.data_ptr(), nb,
+                                                   stream_of(dy))
+                    : ic_conv2d_wgrad_xb(&ax, xb.data_ptr(), &ag, dyb.data_ptr(), k, (int)stride, (int)pad,
+                                         dw.data_ptr<float>(), dbp, (int)math, ws.data_ptr(), nb, stream_of(dy));
+  check_rc(rc, TR ? "conv_transpose2d_wgrad_xb" : "conv2d_wgrad_xb");
+  return {dw, db};
+}
+std::tuple<Tensor, Tensor> conv2d_wgrad_xb(const Tensor& x, const Tensor& xb, const Tensor& dy, const Tensor& dyb,
+                                           const Tensor& w, int64_t stride, int64_t pad, bool bias, int64_t math) {
+  return wgrad_xb<false>(x, xb, dy, dyb, w, stride, pad, bias, math);
+}
+std::tuple<Tensor, Tensor> conv_transpose2d_wgrad_xb(const Tensor& x, const Tensor& xb, const Tensor& dy,
+                                                     const Tensor& dyb, const Tensor& w, int64_t stride, int64_t pad,
+                                                     bool bias, int64_t math) {
+  return wgrad_xb<true>(x, xb, dy, dyb, w, stride, pad, bias, math);
+}
+
 // ---------------------------------------------------------------- elementwise, losses, entropy models
 // Reference interfaces: NonNegativeParam.forward (layers/gdn.py:59-62), Lower/UpperBound
 // (layers/bound.py:28-59), ReLU / torch.abs (prior_analysis.py:65, bmshl2018.py:72), the exp-clamp of
@@ -935,6 +969,16 @@ Tensor conv_transpose2d_fwd_xb_meta(const Tensor& x, const Tensor&, const Tensor
   return conv_transpose2d_fwd_meta(x, w, b, stride, pad, op, act, math);
 }
 
+std::tuple<Tensor, Tensor> conv2d_wgrad_xb_meta(const Tensor& x, const Tensor&, const Tensor& dy, const Tensor&,
+                                                const Tensor& w, int64_t s, int64_t p, bool bias, int64_t m) {
+  return conv2d_wgrad_meta(x, dy, w, s, p, bias, m);
+}
+std::tuple<Tensor, Tensor> conv_transpose2d_wgrad_xb_meta(const Tensor& x, const Tensor&, const Tensor& dy,
+                                                          const Tensor&, const Tensor& w, int64_t s, int64_t p,
+                                                          bool bias, int64_t m) {
+  return conv_transpose2d_wgrad_meta(x, dy, w, s, p, bias, m);
+}
+
 // elementwise / loss / entropy shape kernels
 Tensor like_meta1(const Tensor& x) { return at::empty_like(x, at::MemoryFormat::Preserve); }
 Tensor nonneg_fwd_meta(const Tensor& p, double, double) { return like_meta1(p); }
@@ -1041,6 +1085,10 @@ TORCH_LIBRARY(imgcomp, m) {
   m.def("conv_transpose2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, "
         "int math) -> Tensor");
   m.def("conv2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, int math) -> Tensor");
+  m.def("conv2d_wgrad_xb(Tensor x, Tensor xb, Tensor dy, Tensor dyb, Tensor weight, int stride, int padding, "
+        "bool bias, int math) -> (Tensor, Tensor)");
+  m.def("conv_transpose2d_wgrad_xb(Tensor x, Tensor xb, Tensor dy, Tensor dyb, Tensor weight, int stride, "
+        "int padding, bool bias, int math) -> (Tensor, Tensor)");
   m.def("conv_transpose2d_fwd_xb(Tensor x, Tensor xb, Tensor weight, Tensor? bias, int stride, int padding, "
         "int output_padding, int act, int math) -> Tensor");
   m.def("nonneg_fwd(Tensor p, float bound, float pedestal) -> Tensor");
@@ -1098,6 +1146,8 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb);
   m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb);
+  m.impl("conv2d_wgrad_xb", conv2d_wgrad_xb);
+  m.impl("conv_transpose2d_wgrad_xb", conv_transpose2d_wgrad_xb);
   m.impl("conv_transpose2d_fwd_xb", conv_transpose2d_fwd_xb);
   m.impl("nonneg_fwd", nonneg_fwd);
   m.impl("nonneg_bwd", nonneg_bwd);
@@ -1146,6 +1196,8 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb_meta);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb_meta);
   m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb_meta);
+  m.impl("conv2d_wgrad_xb", conv2d_wgrad_xb_meta);
+  m.impl("conv_transpose2d_wgrad_xb", conv_transpose2d_wgrad_xb_meta);
   m.impl("conv_transpose2d_fwd_xb", conv_transpose2d_fwd_xb_meta);
   m.impl("nonneg_fwd", nonneg_fwd_meta);
   m.impl("nonneg_bwd", nonneg_bwd_meta);

@@ -11,6 +11,8 @@
 // LDS holds BK=16 pixel rows of both operands, channel-contiguous (exactly as
 // they sit in NHWC memory); a half-wave reads 32 consecutive floats of one row
 // per operand fragment (ds_read_b32, conflict-free).
+#include <type_traits>
+
 #include "gemm.h"
 #include <algorithm>
 
@@ -732,6 +734,12 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #ifndef WG_X3P
 #define WG_X3P 1  // the tap-group weight gradients on producer / consumer waves (wg_x3p_kernel); 0: wg_x3g_kernel
 #endif
+#ifndef WG_X3P_DEEP  // bf16-copy producers keep three steps of loads in flight instead of two
+#define WG_X3P_DEEP 1
+#endif
+#ifndef WG_X3P_B16
+#define WG_X3P_B16 1  // bf16 weight gradients read the operands' bf16 copies when the caller passes them (C3)
+#endif
 #ifndef WG_X3P_PRIO
 #define WG_X3P_PRIO 1  // s_setprio of the producer waves (0: hardware default; 1: g_a.2 wgrad 1.163 -> 1.107 ms, r07l)
 #endif
@@ -1193,8 +1201,12 @@ __device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int sp
 // per step for all twelve.  In wg_x3g the split + store of the next step sat in each MFMA wave's
 // instruction stream (0.36 ms of a 1.19 ms g_a.2 wgrad: WG_X3G_ABL, profiles/r06k_*); a producer wave
 // issues its VALU and LDS stores while its SIMD's MFMA pipe is busy with the consumers' work.
-template <bool XSQ, int NTAP, int NP>
+// B16 (with NP = 1, not XSQ): the producers read G and X from their bf16 copies (d.g16, d.x16: 8 B per
+// four values, nothing converted).  The bf16 weight gradient is bound by the producers' loads (no
+// MFMAs: the same time; no loads: half, profiles/r07x_*), so half the bytes is most of what it can gain.
+template <bool XSQ, int NTAP, int NP, bool B16 = false>
 __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int split, int ky, int ct) {
+  static_assert(!B16 || (NP == 1 && !XSQ), "bf16 copies: one plane, plain X");
   typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   constexpr int CW = 192 / NTAP;          // X channels per block
@@ -1241,17 +1253,20 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
       xrow[q] = f / (CW / 4);
       xcol[q] = (f - xrow[q] * (CW / 4)) * 4;
     }
+    constexpr uint32_t ESZ = B16 ? 2u : 4u;  // bytes per element of the operands the producers read
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef typename std::conditional<B16, u32x2, floatx4v>::type slot_t;  // four values
     uint32_t goff[QG];
 #pragma unroll
-    for (int q = 0; q < QG; ++q) goff[q] = ((uint32_t)grow[q] * (uint32_t)d.gs_w + (uint32_t)gcol[q]) * 4u;
-    floatx4v ga[QG] = {}, xa[QX] = {}, gb[QG] = {}, xb[QX] = {};
+    for (int q = 0; q < QG; ++q) goff[q] = ((uint32_t)grow[q] * (uint32_t)d.gs_w + (uint32_t)gcol[q]) * ESZ;
+    slot_t ga[QG] = {}, xa[QX] = {}, gb[QG] = {}, xb[QX] = {};
     uint32_t oka = 0, okb = 0;
     // step k of the block (pixels q0 + k BK ..).  Branch-free: every load reads an in-range address
     // (dead steps pixel 0, padding a clamped column / row) and a select zeroes what must be zero; with
     // a zero-page pointer select the compiler branched around each load on the uniform step flag and
     // drained the loads in flight (s_waitcnt vmcnt(0)) inside the branches.
     // the zeroing select is applied at the store (store()), so no value is consumed before its step
-    auto load = [&](int k, floatx4v (&rg)[QG], floatx4v (&rx)[QX], uint32_t& okm) {
+    auto load = [&](int k, slot_t (&rg)[QG], slot_t (&rx)[QX], uint32_t& okm) {
       if (WG_X3P_ABL & 32) k = 0;  // the first step's addresses every step (hoisted address math, L2-hot)
       const int p0 = q0 + k * BK;
       const bool live = p0 >= pb && p0 < pe;
@@ -1264,18 +1279,20 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
       const bool rowok = live && (unsigned)iy < (unsigned)d.Hx;
       const int iyc = min(max(iy, 0), d.Hx - 1);
       // wave-uniform bases (SGPRs) + 32-bit per-lane byte offsets: the saddr form of global_load
-      const char* gbase = (const char*)(d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w);
-      const char* xbase = (const char*)(d.x + (long long)img * d.xs_n + (long long)iyc * d.xs_h + c0);
+      const long long goe = (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w;
+      const long long xoe = (long long)img * d.xs_n + (long long)iyc * d.xs_h + c0;
+      const char* gbase = B16 ? (const char*)((const __bf16*)d.g16 + goe) : (const char*)(d.g + goe);
+      const char* xbase = B16 ? (const char*)((const __bf16*)d.x16 + xoe) : (const char*)(d.x + xoe);
 #pragma unroll
       for (int q = 0; q < QG; ++q)
-        if (!(WG_X3P_ABL & 1)) rg[q] = *(const floatx4v*)(gbase + goff[q]);
+        if (!(WG_X3P_ABL & 1)) rg[q] = *(const slot_t*)(gbase + goff[q]);
       okm = live ? 1u : 0u;
 #pragma unroll
       for (int q = 0; q < QX; ++q) {
         const int ix = ((int)gx0 + xrow[q]) * 2 + dx0;
         const bool ok = rowok && (unsigned)ix < (unsigned)d.Wx;
         const uint32_t ixc = (uint32_t)min(max(ix, 0), d.Wx - 1);
-        if (!(WG_X3P_ABL & 1)) rx[q] = *(const floatx4v*)(xbase + (ixc * (uint32_t)d.xs_w + (uint32_t)xcol[q]) * 4u);
+        if (!(WG_X3P_ABL & 1)) rx[q] = *(const slot_t*)(xbase + (ixc * (uint32_t)d.xs_w + (uint32_t)xcol[q]) * ESZ);
         okm |= ok ? 2u << q : 0u;
       }
     };
@@ -1292,9 +1309,19 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
       }
     };
     const floatx4v zero4 = {0.f, 0.f, 0.f, 0.f};
-    auto store = [&](int buf, const floatx4v (&rg)[QG], const floatx4v (&rx)[QX], uint32_t okm) {
+    auto store = [&](int buf, const slot_t (&rg)[QG], const slot_t (&rx)[QX], uint32_t okm) {
       if (WG_X3P_ABL & 2) return;
       __bf16* base = lds + buf * STAGE;
+      if constexpr (B16) {  // bf16 copies: four values already rounded, 8 B straight to LDS
+        const u32x2 z2 = {0u, 0u};
+#pragma unroll
+        for (int q = 0; q < QG; ++q)
+          *(u32x2*)(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q]))) = (okm & 1u) ? rg[q] : z2;
+#pragma unroll
+        for (int q = 0; q < QX; ++q)
+          *(u32x2*)(base + GOPER + xrow[q] * PITCH + (xcol[q] ^ swz(xrow[q]))) = (okm & (2u << q)) ? rx[q] : z2;
+        return;
+      } else {
 #pragma unroll
       for (int q = 0; q < QG; ++q) {
         put(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q])), GPLANE, (okm & 1u) ? rg[q] : zero4);
@@ -1307,8 +1334,50 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
         put(base + GOPER + xrow[q] * PITCH + (xcol[q] ^ swz(xrow[q])), XPLANE, v);
         __builtin_amdgcn_sched_barrier(0);
       }
+      }
     };
     const int L = (pe - q0) / BK;  // steps run (even)
+    if constexpr (B16 && WG_X3P_DEEP) {
+      // bf16 slots are half the registers: a third set keeps three steps of loads in flight
+      // (the r07x ablation showed the bf16 kernel waits on its loads, not on its MFMAs)
+      slot_t gc[QG] = {}, xc[QX] = {};
+      uint32_t okc = 0;
+      if (L > 0) {
+        load(0, ga, xa, oka);
+        load(1, gb, xb, okb);
+        load(2, gc, xc, okc);
+        store(0, ga, xa, oka);
+        load(3, ga, xa, oka);
+      }
+      __syncthreads();
+      // at sub-step j the consumers run step j; the producers store step j + 1 and load step j + 4
+      for (int k = 0; k < L; k += 6) {
+        store(1, gb, xb, okb);
+        load(k + 4, gb, xb, okb);
+        __syncthreads();
+        if (k + 1 >= L) break;
+        store(0, gc, xc, okc);
+        load(k + 5, gc, xc, okc);
+        __syncthreads();
+        if (k + 2 >= L) break;
+        store(1, ga, xa, oka);
+        load(k + 6, ga, xa, oka);
+        __syncthreads();
+        if (k + 3 >= L) break;
+        store(0, gb, xb, okb);
+        load(k + 7, gb, xb, okb);
+        __syncthreads();
+        if (k + 4 >= L) break;
+        store(1, gc, xc, okc);
+        load(k + 8, gc, xc, okc);
+        __syncthreads();
+        if (k + 5 >= L) break;
+        store(0, ga, xa, oka);
+        load(k + 9, ga, xa, oka);
+        __syncthreads();
+      }
+      return;
+    }
     if (L > 0) {
       load(0, ga, xa, oka);
       load(1, gb, xb, okb);
@@ -1414,7 +1483,7 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
     for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
 }
 
-template <bool XSQ, int NP = 3>
+template <bool XSQ, int NP = 3, bool B16 = false>
 __global__ void __launch_bounds__(768, 1) wg_x3p_kernel(const WgDesc d) {
   constexpr int STAGE = NP * (32 * 192 + 34 * 192);
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
@@ -1424,8 +1493,8 @@ __global__ void __launch_bounds__(768, 1) wg_x3p_kernel(const WgDesc d) {
   if (wid >= nblk) return;
   const int split = wid / 25, rem = wid - (wid / 25) * 25;
   const int ky = rem / 5, u = rem - (rem / 5) * 5;
-  if (u < 3) wg_x3p_body<XSQ, 3, NP>(d, lds, split, ky, u);
-  else wg_x3p_body<XSQ, 2, NP>(d, lds, split, ky, u - 3);
+  if (u < 3) wg_x3p_body<XSQ, 3, NP, B16>(d, lds, split, ky, u);
+  else wg_x3p_body<XSQ, 2, NP, B16>(d, lds, split, ky, u - 3);
 }
 
 template <bool XSQ, int NP = 3>
@@ -1577,7 +1646,9 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
   if (wg_x3g_ok(d) && WG_X3P) {
-    if (d.bf16) {
+    if (WG_X3P_B16 && d.bf16 && !sq && d.g16 && d.x16) {
+      hipLaunchKernelGGL((wg_x3p_kernel<false, 1, true>), grid, dim3(768), 0, s, d);
+    } else if (d.bf16) {
       if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true, 1>), grid, dim3(768), 0, s, d);
       else hipLaunchKernelGGL((wg_x3p_kernel<false, 1>), grid, dim3(768), 0, s, d);
     } else if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true>), grid, dim3(768), 0, s, d);

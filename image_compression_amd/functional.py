@@ -167,6 +167,7 @@ class Conv2dFn(Function):
         else:
             y = _lib.ops().conv2d_fwd(x, w, b, stride, padding, int(act), int(math))
         _log_plan("conv2d_fwd", x, y, w.shape[2], stride, padding, math)
+        ctx.xb = xb  # x's bf16 copy, for the weight gradient with dy's (conv2d_wgrad_xb)
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
@@ -190,7 +191,11 @@ class Conv2dFn(Function):
                 dx = ops.conv2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
+            xb, ctx.xb = ctx.xb, None
+            if xb is not None and gyb is not None and gyb.stride() == gy.stride():
+                dw, db = ops.conv2d_wgrad_xb(x, xb, gy, gyb, w, stride, padding, has_b and pre is None, math)
+            else:
+                dw, db = ops.conv2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
             _log_plan("conv2d_wgrad", x, gy, k, stride, padding, math)
             db = (db if pre is None else pre) if has_b else None
         return dx, dw, db, None, None, None, None
@@ -213,6 +218,7 @@ class ConvTranspose2dFn(Function):
         else:
             y = _lib.ops().conv_transpose2d_fwd(x, w, b, stride, padding, output_padding, int(act), int(math))
         _log_plan("conv_transpose2d_fwd", x, y, w.shape[2], stride, padding, math)
+        ctx.xb = xb  # x's bf16 copy, for the weight gradient with dy's (conv_transpose2d_wgrad_xb)
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
@@ -236,7 +242,11 @@ class ConvTranspose2dFn(Function):
                 dx = ops.conv_transpose2d_dgrad(gy, w, x, stride, padding, math)
             _log_plan("conv_transpose2d_dgrad", gy, dx, k, stride, padding, math)
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
+            xb, ctx.xb = ctx.xb, None
+            if xb is not None and gyb is not None and gyb.stride() == gy.stride():
+                dw, db = ops.conv_transpose2d_wgrad_xb(x, xb, gy, gyb, w, stride, padding, has_b and pre is None, math)
+            else:
+                dw, db = ops.conv_transpose2d_wgrad(x, gy, w, stride, padding, has_b and pre is None, math)
             _log_plan("conv_transpose2d_wgrad", x, gy, k, stride, padding, math)
             db = (db if pre is None else pre) if has_b else None
         return dx, dw, db, None, None, None, None, None

@@ -183,6 +183,13 @@ int ic_conv_transpose2d_fwd_xb(const ic_act* x, const void* xb, const float* w, 
                                int pad, const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);
 int ic_conv2d_dgrad_xb(const ic_act* dy, const void* dyb, const float* w, int k, int stride, int pad,
                        const ic_act* dx, int math, void* ws, size_t ws_bytes, void* stream);
+/* weight gradients reading both operands' bf16 copies (x's from its producer's forward, dy's from its
+ * producer's backward); workspace from *_wgrad_ws_ex */
+int ic_conv2d_wgrad_xb(const ic_act* x, const void* xb, const ic_act* dy, const void* dyb, int k, int stride, int pad,
+                       float* dw, float* db, int math, void* ws, size_t ws_bytes, void* stream);
+int ic_conv_transpose2d_wgrad_xb(const ic_act* x, const void* xb, const ic_act* dy, const void* dyb, int k,
+                                 int stride, int pad, float* dw, float* db, int math, void* ws, size_t ws_bytes,
+                                 void* stream);
 
 /* ---- launch-plan query: which kernel instance, tile and K / pixel split a conv or GDN op would launch
  *      for these shapes (no launch, no device access; the same decision code as the launching entry

@@ -324,6 +324,15 @@ def _meta_cases():
                            [s, (192, 192), (192,), (192,), s]),
         "conv2d_fwd_xb": (lambda o: o.conv2d_fwd_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5),
                                                     None, 2, 2, 0, 3), [(2, 192, 8, 8)]),
+        "conv2d_wgrad_xb": (lambda o: o.conv2d_wgrad_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16),
+                                                        _meta(2, 192, 8, 8, cl=True),
+                                                        _meta(2, 192, 8, 8, cl=True, dtype=torch.bfloat16),
+                                                        _meta(192, 192, 5, 5), 2, 2, True, 3),
+                            [(192, 192, 5, 5), (192,)]),
+        "conv_transpose2d_wgrad_xb": (lambda o: o.conv_transpose2d_wgrad_xb(
+            _meta(2, 192, 8, 8, cl=True), _meta(2, 192, 8, 8, cl=True, dtype=torch.bfloat16), x,
+            _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5), 2, 2, True, 3),
+                                      [(192, 192, 5, 5), (192,)]),
         "conv2d_dgrad_xb": (lambda o: o.conv2d_dgrad_xb(_meta(2, 192, 8, 8, cl=True),
                                                         _meta(2, 192, 8, 8, cl=True, dtype=torch.bfloat16),
                                                         _meta(192, 192, 5, 5), x, 2, 2, 3), [s]),
