@@ -770,6 +770,12 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D_DMA_J
 #define IG_X3D_DMA_J 4  // DMA_AT 2: before n-tile j's MFMAs (r03zx-r03zy: j = 4 of 12, 1.7-2.7 % per C2 step over 0)
 #endif
+#ifndef IG_X3D_M32
+#define IG_X3D_M32 0  // v_mfma_f32_32x32x16_bf16 wave tiles (ig_kernel_x3d<true>): 18 % slower on g_a.2 fwd (r08a), off
+#endif
+#ifndef IG_X3D_DMA_J32
+#define IG_X3D_DMA_J32 2  // M32: the next chunk's DMA issues before column tile j's MFMAs (of 6)
+#endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
 #endif
@@ -790,8 +796,15 @@ __device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
 
 __device__ __forceinline__ int ig_swa(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
 
+// M32: v_mfma_f32_32x32x16_bf16 on 32 x 192 wave tiles (one 32-row tile, six 32-column tiles, two
+// K steps of 16 per chunk): half the MFMA issues of the 16x16x32 form for the same products, and
+// an MFMA holds the SIMD's vector issue for 8 of its 32 cycles instead of 8 of 16, so the A split's
+// VALU has 1.5x the free issue cycles per FLOP (MI355X_MICROARCH.md).  Same operands, LDS images,
+// DMA and chunk order; the MFMA's internal K-sum is 16 instead of 32, so not bitwise the 16x16 form.
+template <bool M32>
 __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
-  constexpr int BM = 256, BN = 192, WM = IG_X3D_WM, WN = BM * BN / 8 / WM, TM = WM / 16, TN = WN / 16, LDB = 32;
+  constexpr int BM = 256, BN = 192, WM = M32 ? 32 : IG_X3D_WM, WN = BM * BN / 8 / WM, LDB = 32;
+  constexpr int TM = WM / (M32 ? 32 : 16), TN = WN / (M32 ? 32 : 16);
   constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
   constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
   constexpr int STAGE = ASTAGE + BSTAGE;
@@ -868,6 +881,70 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   };
 
   const int wm = w / (BN / WN), wn = w % (BN / WN);
+  int cn = cb / T, tn = cb - (cb / T) * T;  // channel chunk and tap of the next chunk to issue
+  if (cb < ce) {
+    issue(cn, tn, 0);
+    if (++tn == T) { tn = 0; ++cn; }
+  }
+  if constexpr (M32) {
+    // 32x32x16 fragments: lane holds row / column lane & 31, K values 16 ks + 8 h .. + 8 (h = lane >> 5)
+    const int r = lane & 31, h = lane >> 5;
+    int ach[2][2], bch[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      ach[ks][0] = ((4 * ks + 2 * h) ^ ig_swa(r & 15)) << 2;
+      ach[ks][1] = ((4 * ks + 2 * h + 1) ^ ig_swa(r & 15)) << 2;
+      bch[ks] = 8 * ((2 * ks + h) ^ ig_swz(r));
+    }
+    floatx16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    for (int c = cb; c < ce; ++c) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
+      const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
+      bf16x8 a[3][2];
+      const float* ar = As + (wm * WM + r) * 32;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const floatx4v lo = *(const floatx4v*)(ar + ach[ks][0]);
+        const floatx4v hi = *(const floatx4v*)(ar + ach[ks][1]);
+        bf16x4 h0, m0v, l0, h1, m1v, l1;
+        split3_bf16x4(lo, h0, m0v, l0);
+        split3_bf16x4(hi, h1, m1v, l1);
+        a[0][ks] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        a[1][ks] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
+        a[2][ks] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (j == IG_X3D_DMA_J32 && c + 1 < ce) {
+          issue(cn, tn, (c + 1 - cb) & 1);
+          if (++tn == T) { tn = 0; ++cn; }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 b[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 32 + r) * LDB + bch[ks]);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][ks], b[0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[1], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[2], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[1], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[0], acc[j], 0, 0, 0);
+        }
+      }
+    }
+    floatx16 acc2[1][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc2[0][j] = acc[j];
+    ig_epilogue<1, TN>(d, P, acc2, M, m0, 0, wm, wn, WM, WN, r, h, split);
+    return;
+  }
   const int r = lane & 15, g = lane >> 4;
   const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
   const int bch = 8 * (g ^ ig_swz(r));
@@ -877,11 +954,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 
-  int cn = cb / T, tn = cb - (cb / T) * T;  // channel chunk and tap of the next chunk to issue
-  if (cb < ce) {
-    issue(cn, tn, 0);
-    if (++tn == T) { tn = 0; ++cn; }
-  }
   for (int c = cb; c < ce; ++c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1263,7 +1335,10 @@ int ig_run(IgDesc& d, hipStream_t s) {
       if (!d.xb || d.Cin % 64 != 0) return IC_ERR_ARG;
       hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     } else {
-      hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      if (IG_X3D_M32)
+        hipLaunchKernelGGL(ig_kernel_x3d<true>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      else
+        hipLaunchKernelGGL(ig_kernel_x3d<false>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     }
     IC_CHECK_LAUNCH();
     rc = IC_OK;
