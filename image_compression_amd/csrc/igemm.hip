@@ -1138,6 +1138,145 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_b16d(const IgDesc d) {
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
 }
 
+// ig_kernel_b16d's tiles, waves and MFMA order on a ring of S 32-channel slots (A 16 KB + B 12 KB each,
+// 140 KB at S = 5) instead of two 64-channel stages: each chunk's LDS-DMA issues S - 1 chunks ahead of
+// its MFMAs and the wait before a chunk's barrier (s_waitcnt vmcnt(n)) leaves the later chunks in
+// flight.  A two-stage chunk had about 0.7 us of MFMAs per SIMD to hide the DMA issued a third of the
+// way into it (C3's wg_x3p showed the same load latency, r07z).  Chunk c32 runs tap (c32 / 2) % T,
+// channels 64 (c32 / 2T) + 32 (c32 & 1): the MFMAs of every accumulator in b16d's order, so the result
+// is bitwise that kernel's (the plan's chunk ranges stay in 64-channel units).  Rows of 64 B, 16-B
+// pieces XOR ig_swz(row) (as ig_kernel_x3d's B planes): conflict-free ds_read_b128 fragments.
+#ifndef IG_B16R
+#define IG_B16R 0  // measured 21 % slower than ig_kernel_b16d on C3 (r08b: twice the barriers per MFMA), off
+#endif
+#ifndef IG_B16R_S
+#define IG_B16R_S 5
+#endif
+#ifndef IG_B16R_DMA_J
+#define IG_B16R_DMA_J 2  // the DMA of chunk c + S - 1 issues before column tile j's MFMAs of chunk c
+#endif
+// s_waitcnt vmcnt(n), n a wave-uniform multiple of 3 or 4 up to 4 (S - 2)
+__device__ __forceinline__ void ig_wait_vm(int n) {
+  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ void __launch_bounds__(512, 1) ig_kernel_b16r(const IgDesc d) {
+  constexpr int BM = 256, BN = 192, WM = 32, WN = 192, TM = WM / 16, TN = WN / 16, S = IG_B16R_S;
+  static_assert(S >= 2 && S <= 5, "4 (S - 2) outstanding pieces at most 12");
+  constexpr int ASTAGE = BM * 64;  // 16 KB: 256 rows x 32 bf16
+  constexpr int BSTAGE = BN * 64;  // 12 KB: 192 rows x 32 bf16
+  constexpr int STAGE = ASTAGE + BSTAGE;
+  __shared__ __attribute__((aligned(16))) char lds[S * STAGE];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int T = P.T;
+  const int nchunks = T * (d.Cin >> 6);  // 64-channel units, as the plan's kcps
+  const int cb = 2 * (split * d.kcps);
+  const int ce = 2 * min(nchunks, split * d.kcps + d.kcps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+
+  // A: wave w DMAs rows 32w + 16k + (lane >> 2), k < 2 (1 KB = 16 rows of 64 B per piece); lane's
+  // physical piece lane & 3 holds logical piece (lane & 3) ^ ig_swz(row)
+  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+  uint32_t a_off[2];
+  int a_iy[2], a_ix[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = 32 * w + 16 * k + (lane >> 2);
+    const uint32_t m = m0 + row;
+    const bool ok = m < M;
+    const uint32_t mm = ok ? m : 0u;
+    const uint32_t img = fdiv(mm, P.fd_hw);
+    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+    const uint32_t gy = fdiv(rem, P.fd_w);
+    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+    a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
+    a_ix[k] = (int)gx * d.stride;
+    a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
+               8u * (uint32_t)((lane & 3) ^ ig_swz(row));
+  }
+  // B: 12 pieces of 16 rows; wave w DMAs piece w, and waves 0-3 piece 8 + w too
+  const int nbp = w < 4 ? 2 : 1;
+  const int pw = 2 + nbp;  // DMA pieces per chunk of this wave
+  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+  uint32_t b_off[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int rb = 16 * (w + 8 * kb) + (lane >> 2);
+    b_off[kb] = (uint32_t)rb * (uint32_t)d.Cin + 8u * (uint32_t)((lane & 3) ^ ig_swz(rb));
+  }
+  const __bf16* __restrict__ xg = (const __bf16*)d.xb;
+  const int T2 = 2 * T;
+  auto issue = [&](int c, int slot) {
+    const int cn = c / T2, rm = c - cn * T2, t = rm >> 1;
+    const int c32 = 2 * cn + (rm & 1);  // 32-channel block
+    const uint32_t sb = lbase + (uint32_t)(slot * STAGE);
+    const int dy = P.dy[t], dx = P.dx[t];
+    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + c32 * 32);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
+      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+      ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
+                sb + (uint32_t)((2 * w + k) * 1024));
+    }
+    const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + c32 * 32);
+    ig_glds16(wpb + (b_off[0] + boff), sb + (uint32_t)(ASTAGE + w * 1024));
+    if (nbp == 2) ig_glds16(wpb + (b_off[1] + boff), sb + (uint32_t)(ASTAGE + (8 + w) * 1024));
+  };
+
+  const int wm = w, wn = 0;
+  const int r = lane & 15, g = lane >> 4;
+  const int ch = 16 * (g ^ ig_swz(r));
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    if (cb + k < ce) issue(cb + k, k);
+  int slot = 0, islot = S - 1;  // slot of chunk c; slot chunk c + S - 1 goes to
+  for (int c = cb; c < ce; ++c) {
+    // chunk c's pieces landed; the ones of chunks c + 1 .. c + S - 2 may stay in flight
+    ig_wait_vm((min(ce - 1, c + S - 2) - c) * pw);
+    __syncthreads();
+    const char* As = lds + slot * STAGE;
+    const char* Bs = As + ASTAGE;
+    bf16x8 a[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *(const bf16x8*)(As + (wm * WM + i * 16 + r) * 64 + ch);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j == IG_B16R_DMA_J && c + S - 1 < ce) issue(c + S - 1, islot);  // into chunk c - 1's slot
+      const bf16x8 b = *(const bf16x8*)(Bs + (wn * WN + j * 16 + r) * 64 + ch);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
+    }
+    slot = slot == S - 1 ? 0 : slot + 1;
+    islot = islot == S - 1 ? 0 : islot + 1;
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
+}
+
 __global__ void __launch_bounds__(256) ig_cvt_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ xb,
                                                           long long n8) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1333,7 +1472,10 @@ int ig_run(IgDesc& d, hipStream_t s) {
     if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
     if (d.bf16) {
       if (!d.xb || d.Cin % 64 != 0) return IC_ERR_ARG;
-      hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      if (IG_B16R)
+        hipLaunchKernelGGL(ig_kernel_b16r, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      else
+        hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     } else {
       if (IG_X3D_M32)
         hipLaunchKernelGGL(ig_kernel_x3d<true>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
