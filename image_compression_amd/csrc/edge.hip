@@ -1143,7 +1143,13 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
     // input-row stationary: runs of input rows (x column segments past 128), about one block per CU
     const int wseg = Win <= 128 ? Win : TF2_WSEG;
     const long long nseg = (Win + wseg - 1) / wseg;
-    long long run = ((long long)N * Hin * nseg + 255) / 256;
+    // one block per CU (157 KB of LDS): split each (image, segment) row sequence into as many runs as
+    // keep the grid within 256 blocks, so the grid runs in one round.  Rounding the row count per block
+    // up instead (r08d: C5's 16 x 3 sequences of 256 rows in runs of 48 = 288 blocks) left 32 blocks
+    // for a second round of full-length runs: 0.73 ms for C5's g_s.6 forward.
+    const long long units = (long long)N * nseg;
+    const long long per = units < 256 ? 256 / units : 1;
+    long long run = (Hin + per - 1) / per;
     if (run < 4) run = 4;
     if (run > Hin) run = Hin;
     const long long blocks = (long long)N * ((Hin + run - 1) / run) * nseg;
