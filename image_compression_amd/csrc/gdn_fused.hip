@@ -66,6 +66,12 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef GDN_BWD_X3W_BF16
 #define GDN_BWD_X3W_BF16 0  // 1: C3's GDN backward (bf16 operands) on gdn_bwd_x3w_kernel<192, INV, 1> (r07u: 0.341 vs 0.333 ms at 128^2, C3 -1 %); 0: gdn_bwd_fused_kernel
 #endif
+#ifndef X3W_LATE
+#define X3W_LATE 0  // gdn_bwd_x3w_kernel: phase A's last part in the dgamma GEMM's MFMA shadows (r08f: 12-14 VGPRs spilled, 0.49 -> 0.55 ms at 128^2), off
+#endif
+#ifndef X3W_LATE_V
+#define X3W_LATE_V 5  // X3W_LATE: VALU per 32x32x16 MFMA in the dgamma section's schedule
+#endif
 #ifndef X3W_SGB
 #define X3W_SGB 1  // gdn_bwd_x3w_kernel: interleave phase A / epilogue with the MFMAs (sched_group_barrier)
 #endif
@@ -1106,7 +1112,7 @@ __global__ void __launch_bounds__(256, 1)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][st], cur[0], acc[j], 0, 0, 0);
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[0], acc[j], 0, 0, 0);
           }
-          pa_slice(pr, 3 * h2 + j);
+          if (!(X3W_LATE && pr == K32 / 2 - 1)) pa_slice(pr, 3 * h2 + j);
           if (X3W_SGB) {
 #pragma unroll
             for (int k = 0; k < (NP == 1 ? 1 : 6); ++k) {
@@ -1160,12 +1166,18 @@ __global__ void __launch_bounds__(256, 1)
         }
         acc_s[3 + j][tid] += d;
       }
+      // X3W_LATE: the last part of phase A(t+G) here, two slices per column group, in the free issue
+      // cycles of the 32x32x16 MFMAs (24 of 32 each) instead of the dx GEMM's 16x16x32 shadows (8 of 16)
+      if (X3W_LATE) {
+        pa_slice(K32 / 2 - 1, 2 * j);
+        pa_slice(K32 / 2 - 1, 2 * j + 1);
+      }
       if (X3W_SGB) {
 #pragma unroll
         for (int k = 0; k < (NP == 1 ? 3 : 18); ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
           if (k < 6) __builtin_amdgcn_sched_group_barrier(0x100, NP == 1 ? 2 : 1, 0);  // DS read (the next bb)
-          __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : 2, 0);  // VALU
+          __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : (X3W_LATE ? X3W_LATE_V : 2), 0);  // VALU
         }
       }
       __builtin_amdgcn_sched_barrier(0);

@@ -106,6 +106,7 @@ def test_tconv_split_fwd_dgrad(n, c, h, w, k, s, p, op):
     (1, 192, 6, 130),                # rows wider than one block: two column segments
     (1, 192, 5, 384),                # the Kodak landscape g_s.6 width (512x768 image): 4 segments
     (2, 80, 4, 250),                 # segments on the fp32 input-row kernel, ragged last segment
+    (16, 192, 32, 250),              # C5's grid shape: 48 row sequences, runs of 7 rows (ragged last run)
 ])
 def test_tconv_few_split(n, cin, h, w):
     """The input-row-stationary transposed conv to a few-channel image (tconv_few2_kernel) in
