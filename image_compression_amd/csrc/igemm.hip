@@ -1004,6 +1004,156 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
 }
 
+// ig_kernel_x3d with the LDS-DMA on producer waves (IG_X3D_PC): 12 waves, the 8 consumer waves only
+// read fragments, split A and run the MFMAs (x3d's wave tiles and order: bitwise its result), and one
+// producer wave per SIMD issues all 68 DMA pieces of the next chunk (17 each) right after the chunk's
+// barrier and waits for them before the next.  An LDS-DMA piece costs its issuing wave 60-185 cycles
+// (MI355X_MICROARCH.md), 8.5 pieces per chunk on each MFMA wave in x3d; here no MFMA wave issues one.
+// Three waves per SIMD: the consumers must fit 168 registers (x3d's waves hold 217 with the DMA
+// addresses).
+#ifndef IG_X3D_PC
+#define IG_X3D_PC 0  // measured 5 % slower per C2 step than ig_kernel_x3d (r08g), off
+#endif
+__global__ void __launch_bounds__(768, 1) ig_kernel_x3pc(const IgDesc d) {
+  constexpr int BM = 256, BN = 192, WM = 32, WN = 192, LDB = 32;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
+  constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
+  constexpr int STAGE = ASTAGE + BSTAGE;
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int zi = blockIdx.z;
+  const int phase = zi / d.ksplit;
+  const int split = zi - phase * d.ksplit;
+  const IgPhase& P = d.ph[phase];
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  if ((int)bx >= P.mtiles) return;
+  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
+  const uint32_t m0 = bx * BM;
+  const int T = P.T;
+  const int nchunks = T * (d.Cin >> 5);
+  const int cb = split * d.kcps;
+  const int ce = min(nchunks, cb + d.kcps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  if (w >= 8) {
+    // ---------------------------------------------------------------- producer waves
+    const int pw = w - 8;
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+    // A: producer pw DMAs pieces 8 pw + k (k < 8), rows 8 (8 pw + k) + (lane >> 3); lane's physical
+    // chunk lane & 7 holds logical chunk (lane & 7) ^ ig_swa(row)
+    const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
+    uint32_t a_off[8];
+    int a_iy[8], a_ix[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = 64 * pw + 8 * k + (lane >> 3);
+      const uint32_t m = m0 + row;
+      const bool ok = m < M;
+      const uint32_t mm = ok ? m : 0u;
+      const uint32_t img = fdiv(mm, P.fd_hw);
+      const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
+      const uint32_t gy = fdiv(rem, P.fd_w);
+      const uint32_t gx = rem - gy * (uint32_t)P.Wg;
+      a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
+      a_ix[k] = (int)gx * d.stride;
+      a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
+                 4u * (uint32_t)((lane & 7) ^ ig_swa(row & 15));
+    }
+    // B: producer pw DMAs pieces jj = pw + 4 kb (kb < 9): plane jj / 12, rows 16 (jj % 12) + (lane >> 2)
+    const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
+    uint32_t b_off[9];
+#pragma unroll
+    for (int kb = 0; kb < 9; ++kb) {
+      const int jj = pw + 4 * kb;
+      const int q = jj / 12, rb = 16 * (jj - 12 * q) + (lane >> 2);
+      b_off[kb] = (uint32_t)q * (uint32_t)d.wplane + (uint32_t)rb * (uint32_t)d.Cin +
+                  8u * (uint32_t)((lane & 3) ^ ig_swz(rb));
+    }
+    const float* __restrict__ xg = d.x;
+    auto issue = [&](int cc, int t, int st) {
+      const uint32_t sb = lbase + (uint32_t)(st * STAGE);
+      const int dy = P.dy[t], dx = P.dx[t];
+      const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
+        const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
+        ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
+                  sb + (uint32_t)((8 * pw + k) * 1024));
+      }
+      const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 32);
+#pragma unroll
+      for (int kb = 0; kb < 9; ++kb) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (pw + 4 * kb) * 1024));
+    };
+    int cn = cb / T, tn = cb - (cb / T) * T;
+    if (cb < ce) {
+      issue(cn, tn, 0);
+      if (++tn == T) { tn = 0; ++cn; }
+    }
+    for (int c = cb; c < ce; ++c) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // chunk c published; stage (c + 1) & 1 free (chunk c - 1 done)
+      if (c + 1 < ce) {
+        issue(cn, tn, (c + 1 - cb) & 1);
+        if (++tn == T) { tn = 0; ++cn; }
+      }
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ consumer waves (x3d's loop)
+  const int wm = w, wn = 0;
+  const int r = lane & 15, g = lane >> 4;
+  const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
+  const int bch = 8 * (g ^ ig_swz(r));
+  floatx4v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  for (int c = cb; c < ce; ++c) {
+    __syncthreads();
+    const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
+    const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
+    bf16x8 a[3][TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* ar = As + (wm * WM + i * 16 + r) * 32;
+      const floatx4v lo = *(const floatx4v*)(ar + ach0);
+      const floatx4v hi = *(const floatx4v*)(ar + ach1);
+      bf16x4 h0, m0v, l0, h1, m1v, l1;
+      split3_bf16x4(lo, h0, m0v, l0);
+      split3_bf16x4(hi, h1, m1v, l1);
+      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 16 + r) * LDB + bch);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+      }
+      // at most the next column tile's B fragments ahead: 168 registers hold 96 accumulators, the
+      // split A fragments and two B fragment sets, not all twelve
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
+}
+
 // bf16 operands on 256 x 192 DMA tiles (C3, round 5): ig_kernel_x3d's block, waves, DMA pipeline and
 // epilogue with both operands already bf16 in HBM -- the activations as a compact NHWC bf16 copy (d.xb)
 // and one packed bf16 weight plane -- so nothing is converted or staged through registers.  K chunks of
@@ -1477,7 +1627,9 @@ int ig_run(IgDesc& d, hipStream_t s) {
       else
         hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     } else {
-      if (IG_X3D_M32)
+      if (IG_X3D_PC)
+        hipLaunchKernelGGL(ig_kernel_x3pc, dim3(mt, 1, d.nphase * d.ksplit), dim3(768), 0, s, d);
+      else if (IG_X3D_M32)
         hipLaunchKernelGGL(ig_kernel_x3d<true>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
       else
         hipLaunchKernelGGL(ig_kernel_x3d<false>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
