@@ -288,6 +288,55 @@ def cpu_baseline(seconds_target=12.0):
                       f"(oracle/ref_cpu.py, torch CPU, {threads} threads)"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, env, visible, argv, port=None):
+    """What `bench.py --gpus N` does before anything touches the GPU.
+
+    Returns ("run", None) when this process is the (only) rank to run: N == 1 outside a
+    torch.distributed.run launch, or a launched rank whose WORLD_SIZE equals N.  Returns
+    ("launch", cmd) when N > 1 and WORLD_SIZE is unset: the parent starts cmd -- N ranks
+    under torch.distributed.run on 127.0.0.1 -- as a child process (never an exec), relays
+    rank 0's JSON line and exits with the children's return code.  The reference reaches
+    every visible GPU from one command (engine/trainer.py:256-258, nn.DataParallel); this
+    is that entry point with one process per GPU.  Raises SystemExit (non-zero) when the
+    world cannot be the one asked for: WORLD_SIZE != N, N < 1, or N above the visible
+    devices under RCCL (gloo over GPU tensors, IMGCOMP_DIST_BACKEND=gloo, may share one GPU
+    between ranks -- a rehearsal, never a measurement of N GPUs).  `visible` is
+    torch.cuda.device_count(), which does not initialise the GPU on this image."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} < 1")
+    backend = env.get("IMGCOMP_DIST_BACKEND", "nccl")
+    if gpus > 1 and backend == "nccl" and gpus > visible:
+        raise SystemExit(f"bench.py: --gpus {gpus} but {visible} visible GPU(s): RCCL needs one GPU per rank "
+                         "(no silent smaller run)")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port or _free_port()}", os.path.abspath(__file__)]
+    return "launch", cmd + list(argv)
+
+
+def _launch_children(cmd):
+    """Run the N-rank launch as a child process; rank 0's JSON line passes through on stdout."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "8")
+    proc = subprocess.run(cmd, env=env)
+    return proc.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,6 +361,9 @@ def main():
                     help="run the hyperprior branch on the main stream (Compressor2018.concurrent_hyperprior "
                          "= False; bitwise the same arithmetic)")
     args = ap.parse_args()
+    what, cmd = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), sys.argv[1:])
+    if what == "launch":
+        sys.exit(_launch_children(cmd))
     conf = dict(CONFIGS[args.config])
     if args.math:
         conf["math"] = args.math

@@ -84,6 +84,9 @@ def _comm_stream_allreduce_hook(state, bucket):
     comm = state.comm
     for s in state.streams:
         comm.wait_stream(s)
+    # and the stream current at hook time (a step run under another stream than the one current at
+    # wrap() still has its bucket's gradients followed)
+    comm.wait_stream(torch.cuda.current_stream(comm.device))
     buf = bucket.buffer()
     with torch.cuda.stream(comm):
         buf.div_(state.world)

@@ -167,7 +167,9 @@ class Conv2dFn(Function):
         else:
             y = _lib.ops().conv2d_fwd(x, w, b, stride, padding, int(act), int(math))
         _log_plan("conv2d_fwd", x, y, w.shape[2], stride, padding, math)
-        ctx.xb = xb  # x's bf16 copy, for the weight gradient with dy's (conv2d_wgrad_xb)
+        # x's bf16 copy, for the weight gradient with dy's (conv2d_wgrad_xb); held to the backward
+        # (2 B per element of x) only when that weight gradient will run
+        ctx.xb = xb if ctx.needs_input_grad[1] else None
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
@@ -218,7 +220,9 @@ class ConvTranspose2dFn(Function):
         else:
             y = _lib.ops().conv_transpose2d_fwd(x, w, b, stride, padding, output_padding, int(act), int(math))
         _log_plan("conv_transpose2d_fwd", x, y, w.shape[2], stride, padding, math)
-        ctx.xb = xb  # x's bf16 copy, for the weight gradient with dy's (conv_transpose2d_wgrad_xb)
+        # x's bf16 copy, for the weight gradient with dy's (conv_transpose2d_wgrad_xb); held to the backward
+        # (2 B per element of x) only when that weight gradient will run
+        ctx.xb = xb if ctx.needs_input_grad[1] else None
         ctx.conf = (stride, padding, act, b is not None, int(math))
         ctx.save_for_backward(x, w, y if act else None)
         return y
@@ -476,7 +480,8 @@ class GDNFn(Function):
         b = beta.contiguous()
         # xb & 1: y's bf16 copy for the next conv's forward; xb & 2: dx's for the previous
         # transposed conv's input gradient (bf16 operands only; see _put_bf16)
-        if (xb & 1) and (int(math_fwd) & MATH["bf16"]):
+        # (not under the eval weight cache: its convs (_cached_conv) never take the copy)
+        if (xb & 1) and (int(math_fwd) & MATH["bf16"]) and not _wcache_on(x):
             y, norm, yb = _lib.ops().gdn_fwd_xb(x, g, b, bool(inverse), int(math_fwd))
             _put_bf16(y, yb)
         else:

@@ -59,6 +59,24 @@ def _worker(rank, world, port, outdir):
         torch.cuda.synchronize()
         ddp_grads[conc] = {n: p.grad.detach().cpu() for n, p in model.module.named_parameters()}
         del model, losses
+    # the concurrent DDP step run under another stream than the one current at wrap(): the hook also
+    # follows the stream current at hook time (torch syncs the mismatched accumulations itself; its
+    # warning about them is expected here)
+    torch.manual_seed(0)
+    model = D.wrap(modelling.build_model(_cfg()).to(dev).train(), dev, bucket_cap_mb=4.0, concurrent=True)
+    other = torch.cuda.Stream(device=dev)
+    other.wait_stream(torch.cuda.current_stream(dev))
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="(?s).*AccumulateGrad node's stream does not match")
+        with torch.cuda.stream(other):
+            for _ in range(3):
+                model.zero_grad(set_to_none=True)
+                with injected_noise([uz, uy]):
+                    _, losses = model(x)
+                losses["total_loss"].backward()
+    torch.cuda.synchronize()
+    ddp_grads["other"] = {n: p.grad.detach().cpu() for n, p in model.module.named_parameters()}
+    del model, losses
     # the hipGraph-capable step without DDP: gradients as views of one flat buffer, one
     # all-reduce after the backward, hyperprior side stream on
     torch.manual_seed(0)
@@ -75,7 +93,8 @@ def _worker(rank, world, port, outdir):
     keys = [torch.zeros_like(key) for _ in range(world)]
     torch.distributed.all_gather(keys, key)
     if rank == 0:
-        torch.save({"ddp": ddp_grads[True], "ddp_serial": ddp_grads[False], "flat": flat_grads,
+        torch.save({"ddp": ddp_grads[True], "ddp_serial": ddp_grads[False], "ddp_other": ddp_grads["other"],
+                    "flat": flat_grads,
                     "keys": [int(k) for k in keys], "seed": noise._st().seed}, os.path.join(outdir, "g.pt"))
     D.teardown()
 
@@ -99,6 +118,7 @@ def test_ddp_two_ranks_match_full_batch(tmp_path):
     # the concurrent-hyperprior DDP step (the measured step) is bitwise the single-stream one
     for n in res["ddp"]:
         assert torch.equal(res["ddp"][n], res["ddp_serial"][n]), n
+        assert torch.equal(res["ddp_other"][n], res["ddp_serial"][n]), n
     for kind in ("ddp", "flat"):
         g = res[kind]
         worst = max((rel_err(g[n], p.grad.cpu()), n) for n, p in model.named_parameters())
