@@ -32,6 +32,10 @@ namespace {
 #ifndef EC_SPLIT
 #define EC_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in the edge conv (edge_conv_x3_kernel)
 #endif
+#ifndef EC_ABL
+#define EC_ABL 0  // diagnostic ablations of edge_conv_x3_kernel (wrong results): 1 no output stores, 2 no patch loads,
+                  // 3 no MFMAs, 4 no plane build, 5 neither stores nor loads
+#endif
 #ifndef EW_SPLIT
 #define EW_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in edge_wgrad_kernel
 #endif
@@ -353,8 +357,8 @@ __global__ void __launch_bounds__(512, 1)
     // buffer it & 1 (the previous iteration's) is done
     __syncthreads();
     const long long u2 = u + 2 * gs;
-    edge_patch_load(g, pm, min(u2, ulast), pr);
-    build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
+    if (EC_ABL != 2 && EC_ABL != 5) edge_patch_load(g, pm, min(u2, ulast), pr);  // EC_ABL 2: no patch loads
+    if (EC_ABL != 4) build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
     const __bf16* planes = bpl + (it & 1) * NP * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
@@ -363,7 +367,7 @@ __global__ void __launch_bounds__(512, 1)
       for (int j = 0; j < NTW; ++j) acc[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int sx = 0; sx < EC3_S; ++sx) {
-      if (sx < S) {
+      if (sx < S && EC_ABL != 3) {  // EC_ABL 3: no MFMAs
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int p = 16 * (mt0 + t) + li;
@@ -410,7 +414,7 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ox = seg * SEG + 16 * (mt0 + t) + li;
-      if (ox < g.Wo) {
+      if (ox < g.Wo && ((EC_ABL != 1 && EC_ABL != 5) || ob[t][0][0] == 1234.5678f)) {  // EC_ABL 1: (almost) no stores
 #pragma unroll
         for (int j = 0; j < NTW; ++j) *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = ob[t][j];
       }

@@ -776,6 +776,10 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D_DMA_J32
 #define IG_X3D_DMA_J32 2  // M32: the next chunk's DMA issues before column tile j's MFMAs (of 6)
 #endif
+#ifndef IG_X3D_ABL
+#define IG_X3D_ABL 0  // diagnostic ablations of ig_kernel_x3d<false> (wrong results): 1 = no A split, 2 = no DMA, 3 = no wait for
+                      // the DMA, 4 = no B DMA, 5 = no A DMA
+#endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
 #endif
@@ -863,11 +867,13 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   }
   const float* __restrict__ xg = d.x;
   auto issue = [&](int cc, int t, int st) {
+    if (IG_X3D_ABL == 2) return;  // diagnostic: no DMA
     const uint32_t sb = lbase + (uint32_t)(st * STAGE);
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      if (IG_X3D_ABL == 5) break;  // diagnostic: no A DMA
       const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
       const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
       ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
@@ -876,6 +882,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 32);
 #pragma unroll
     for (int kb = 0; kb < 5; ++kb) {
+      if (IG_X3D_ABL == 4) break;  // diagnostic: no B DMA
       if (w + 8 * kb < NB) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (w + 8 * kb) * 1024));
     }
   };
@@ -955,7 +962,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 
   for (int c = cb; c < ce; ++c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (IG_X3D_ABL != 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ABL 3: diagnostic, no wait
     __syncthreads();
     const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
     const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
@@ -970,8 +977,17 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       const floatx4v lo = *(const floatx4v*)(ar + ach0);
       const floatx4v hi = *(const floatx4v*)(ar + ach1);
       bf16x4 h0, m0v, l0, h1, m1v, l1;
+#if IG_X3D_ABL == 1
+      // diagnostic (wrong results): one conversion per value instead of the split
+      {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        h0 = m0v = l0 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3])});
+        h1 = m1v = l1 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
+      }
+#else
       split3_bf16x4(lo, h0, m0v, l0);
       split3_bf16x4(hi, h1, m1v, l1);
+#endif
       a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
       a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
       a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);

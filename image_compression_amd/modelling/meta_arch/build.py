@@ -22,12 +22,13 @@ def set_compute_dtype(model, dtype):
     (functional.MATH) — for the forward, input gradient and weight gradient of
     every wide conv (g_a, g_s, h_a, h_s).  "bf16": bf16 operands with fp32
     accumulation (reduced precision, BASELINE config C3) for the forward, input
-    gradient and weight gradient of the main transforms (g_a, g_s; their 3-channel
-    image edges too when the library is built with EDGE_BF16) — 97 % of the model's
-    FLOPs; where a bf16 kernel does not apply (weight gradients of maps
-    narrower than 16) they fall back to "fp32_split", and the hyperprior
-    transforms (1.3 % of the FLOPs, but they shape the rate term's gradients)
-    run in "fp32_split" arithmetic there.  GDN and
+    gradient and weight gradient of every wide conv (g_a, g_s, h_a, h_s; the 3-channel
+    image edges too when the library is built with EDGE_BF16); where a bf16 kernel does
+    not apply (weight gradients of maps narrower than 16) they fall back to
+    "fp32_split".  Round 6 moved C3's hyperprior convs from "fp32_split" to bf16
+    operands: their split GEMMs ran on the side stream beside g_s / g_a and took
+    CU time from them (C3 5,430 -> 5,675 images/s alternating on one box,
+    profiles/r09b_c3_hyper_bf16_ab.txt).  GDN and
     the entropy models compute in fp32 in every mode, except that "fp32_split"
     runs GDN (C = 192) in split arithmetic too:
     the fused forward (GDN.math_fwd = 2: 0.37 -> 0.30 ms at 128^2) and the fused
@@ -44,7 +45,7 @@ def set_compute_dtype(model, dtype):
     # IC_MATH_* per transform: bf16 (C3) falls back to split arithmetic (fp32-accurate,
     # faster than the fp32 MFMA) where no bf16 kernel applies, and runs the hyperprior split
     split = MATH["fp32_split"]
-    flags = {"fp32": (0, 0), "fp32_split": (split, split), "bf16": (MATH["bf16"] | split, split)}[dtype]
+    flags = {"fp32": (0, 0), "fp32_split": (split, split), "bf16": (MATH["bf16"] | split, MATH["bf16"] | split)}[dtype]
     for m in model.modules():
         if isinstance(m, (Conv2d, ConvTranspose2d, GDN)):
             m.math = 0

@@ -236,25 +236,28 @@ def synthesis(P, x, strides=(2, 2, 2, 2), k=5, prefix="synthesis_transform.layer
     return x
 
 
-def hyper_analysis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_analysis._layers.", relu_ctl=None):
+def hyper_analysis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_analysis._layers.", relu_ctl=None,
+                   bf16=None):
     """modelling/blocks/prior_analysis.py:43-71: conv, ReLU, conv, ReLU, conv
-    (no bias on the last conv)."""
+    (no bias on the last conv).  bf16: see _conv."""
     n = len(strides)
     for i, (s, k) in enumerate(zip(strides, kernels)):
         b = P.get(f"{prefix}{2*i}.bias") if i < n - 1 else None
-        x = F.conv2d(x, P[f"{prefix}{2*i}.weight"], b, stride=s, padding=k // 2)
+        name = f"{prefix}{2*i}.weight"
+        x = _conv(x, P[name], b, s, k // 2, name, bf16)
         if i < n - 1:
             x = _relu(x, relu_ctl)
     return x
 
 
-def hyper_synthesis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_synthesis._layers.", relu_ctl=None):
+def hyper_synthesis(P, x, strides=(1, 2, 2), kernels=(3, 5, 5), prefix="prior_synthesis._layers.", relu_ctl=None,
+                    bf16=None):
     """modelling/blocks/prior_synthesis.py:44-72: reversed kernels/strides,
-    conv_transpose + ReLU, last layer then clamp(exp(.), 1e-10, 1e10)."""
+    conv_transpose + ReLU, last layer then clamp(exp(.), 1e-10, 1e10).  bf16: see _conv."""
     n = len(strides)
     for i, (s, k) in enumerate(zip(reversed(strides), reversed(kernels))):
-        x = F.conv_transpose2d(x, P[f"{prefix}{2*i}.weight"], P[f"{prefix}{2*i}.bias"],
-                               stride=s, padding=k // 2, output_padding=s - 1)
+        name = f"{prefix}{2*i}.weight"
+        x = _conv(x, P[name], P[f"{prefix}{2*i}.bias"], s, k // 2, name, bf16, transposed=True, opad=s - 1)
         if i < n - 1:
             x = _relu(x, relu_ctl)
     return torch.clamp(x.exp(), 1e-10, 1e10)
@@ -463,14 +466,14 @@ def forward(P, x, u_z=None, u_y=None, train=True, cond="laplace",
             bf16=None, sym_z=None, sym_y=None):
     """modelling/meta_arch/bmshl2018.py:68-98 Compressor2018.forward.
     Returns dict of intermediates and the loss dict.  bf16: per-layer bf16 operand
-    emulation of the main transforms' GEMMs (_conv; None = exact).  sym_z / sym_y (eval):
+    emulation of the convolutions' GEMMs (_conv; None = exact).  sym_z / sym_y (eval):
     symbols fed in place of round(z) / round(y) (see factorized)."""
     N, C, H, W = x.shape
     num_pixels = N * H * W
     y = analysis(P, x, strides, bf16=bf16)
-    z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl)
+    z = hyper_analysis(P, torch.abs(y), hp_strides, hp_kernels, relu_ctl=relu_ctl, bf16=bf16)
     z_tilde, p_z, ce_z = factorized(P, z, u_z, train, bin_, sym=sym_z)
-    sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl)
+    sigma = hyper_synthesis(P, z_tilde, hp_strides, hp_kernels, relu_ctl=relu_ctl, bf16=bf16)
     y_tilde, p_y = conditional(y, sigma, u_y, train, cond, bin_=bin_, sym=sym_y)
     ce_y = ce_loss(p_y)
     x_raw = synthesis(P, y_tilde, strides, bf16=bf16)

@@ -140,7 +140,7 @@ def edges_bf16():
 
 
 def c3_bf16_flags(n, size, latent, edges=None):
-    """Which GEMMs of the main transforms take bf16 operands in the "bf16" compute dtype
+    """Which GEMMs of the convolutions take bf16 operands in the "bf16" compute dtype
     (BASELINE config C3), per weight name: (forward, input gradient, weight gradient) — the
     rule of csrc/conv_api.hip and csrc/wgrad.hip wg_plan, restated: conv / transposed-conv
     forward and input gradient on the implicit GEMM when the reduction channels are a multiple
@@ -171,6 +171,21 @@ def c3_bf16_flags(n, size, latent, edges=None):
         f = (cin % 64 == 0 and (e or cout > 4), cout % 64 == 0 or (e and cout <= 4),
              (e and cout <= 4) or (cout > 4 and wg_ok(cin, cout, wi, n * wi * wi)))
         flags[f"synthesis_transform.layers.{2 * i}.weight"] = f
+        launches += sum(f)
+    # the hyperprior (round 6): every forward and input gradient (reduction channels 192 or the
+    # latent, multiples of 64); the weight gradients of the two 16-wide 3x3 layers by the same rule
+    s16 = size // 16
+    hyp = (("prior_analysis._layers.0.weight", s16, latent, 192), ("prior_analysis._layers.2.weight", s16 // 2, 192, 192),
+           ("prior_analysis._layers.4.weight", s16 // 4, 192, 192))
+    for nm, wo, cin, cout in hyp:  # conv: G = dy (cout channels) on the output grid wo
+        f = (cin % 64 == 0, cout % 64 == 0, wg_ok(cout, cin, wo, n * wo * wo))
+        flags[nm] = f
+        launches += sum(f)
+    hyp = (("prior_synthesis._layers.0.weight", s16 // 4, 192, 192), ("prior_synthesis._layers.2.weight", s16 // 2, 192, 192),
+           ("prior_synthesis._layers.4.weight", s16, 192, latent))
+    for nm, wi, cin, cout in hyp:  # transposed conv: the roles of conv wgrad with x on the input grid wi
+        f = (cin % 64 == 0, cout % 64 == 0, wg_ok(cin, cout, wi, n * wi * wi))
+        flags[nm] = f
         launches += sum(f)
     # every GDN (C = 192, NHWC-dense: the fused kernels) has a bf16 forward and backward
     for t in ("analysis_transform", "synthesis_transform"):

@@ -7,8 +7,8 @@ output pixels, i.e. at the BASELINE configurations' batch sizes.  These tests
   * check single layers at C2 shapes (16 x 192 x 128^2 convs, 16 x 192 x 64^2
     transposed convs) against fp64 torch, asserting the plan they ran;
   * run one whole training step per BASELINE config against the fp64 oracle --
-    at the benchmark's own batch for C2 / C3 / C4 (32, 32, 16 x 256^2), at 4 x 512^2
-    for C5 -- and assert that every kernel instance the benchmark's batch
+    at the benchmark's own batch for C2 / C3 / C4 / C5 (32, 32, 16 x 256^2 and 16 x 512^2)
+    -- and assert that every kernel instance the benchmark's batch
     launches (recorded through functional.record_plans on a bench-size step)
     was launched by the test step.  The oracle takes the HIP path's
     hyperprior ReLU masks; a mask may differ only where the pre-activation is
