@@ -32,10 +32,6 @@ namespace {
 #ifndef EC_SPLIT
 #define EC_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in the edge conv (edge_conv_x3_kernel)
 #endif
-#ifndef EC_ABL
-#define EC_ABL 0  // diagnostic ablations of edge_conv_x3_kernel (wrong results): 1 no output stores, 2 no patch loads,
-                  // 3 no MFMAs, 4 no plane build, 5 neither stores nor loads
-#endif
 #ifndef EW_SPLIT
 #define EW_SPLIT 1  // split arithmetic (IC_MATH_SPLIT) in edge_wgrad_kernel
 #endif
@@ -47,6 +43,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __attribute__((aligned(16))) float edge_zero_page[4];
+__device__ __attribute__((aligned(16))) float edge_store_dump[128];  // written, never read
 
 struct EdgeGeom {
   const float* x;            // few-channel image, NCHW strides (sw == 1)
@@ -120,6 +117,43 @@ __device__ __forceinline__ void edge_patch_store(const EdgeGeom& g, const float 
   for (int q = 0; q < EdgePatchMapT<NT>::R; ++q) {
     const int i = tid + NT * q;
     patch[i < tot ? i : tot] = pr[q];  // pr = 0 past the patch
+  }
+}
+
+// The patch of unit u straight into LDS (global_load_lds_dword: each wave-instruction writes 64
+// consecutive floats at M0 + 4 lane), element i = tid + 512 q as edge_patch_load / _store<512> place
+// it; instructions whose 64 elements all lie past the patch are skipped (wave-uniform), the lanes of a
+// partial one load the zero page into the zero run that follows the patch.  Counted by vmcnt like any
+// load; the caller waits for it.
+__device__ __forceinline__ void edge_patch_dma(const EdgeGeom& g, const EdgePatchMapT<512>& m, long long u,
+                                               uint32_t buf_lds, int w) {
+  const unsigned uu = (unsigned)u, upr = (unsigned)g.units_per_row, ho = (unsigned)g.Ho;
+  const unsigned r = uu / upr;
+  const int seg = (int)(uu - r * upr);
+  const unsigned n = r / ho;
+  const int oy = (int)(r - n * ho);
+  const int iy0 = oy * g.stride - g.pad, ix0 = seg * SEG * g.stride - g.pad;
+  const float* xb = g.x + (long long)n * g.sn;
+  const int sc = (int)g.sc, sh = (int)g.sh;
+  const int tot = g.C * g.k * g.PW;
+#pragma unroll
+  for (int q = 0; q < EdgePatchMapT<512>::R; ++q) {
+    if (64 * w + 512 * q >= tot) break;
+    const int pk = m.pk[q];
+    const int iy = iy0 + ((pk >> 9) & 7), ix = ix0 + (pk & 511);
+    const bool ok = pk >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    const float* src = ok ? xb + ((pk >> 12) * sc + iy * sh + ix) : (const float*)edge_zero_page;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(buf_lds + 4u * (uint32_t)(64 * w + 512 * q));
+    uint32_t save;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(save)
+        : "v"(src), "s"(dst)
+        : "memory");
   }
 }
 
@@ -334,14 +368,14 @@ __global__ void __launch_bounds__(512, 1)
   EdgePatchMapT<512> pm;
   edge_patch_map(g, pm, tid);
   const long long u0 = blockIdx.x, gs = gridDim.x, ulast = g.units - 1;
-  float pr[EdgePatchMapT<512>::R];
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index, known uniform (the DMA's skip is a scalar branch)
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds);
   // prologue: patch(u0) -> buffer 0, planes(u0) -> plane buffer 0, patch(u0 + gs) -> buffer 1
-  edge_patch_load(g, pm, u0, pr);
-  edge_patch_store<512>(g, pr, lds, tid);
+  edge_patch_dma(g, pm, u0, lds0, wu);
+  edge_patch_dma(g, pm, min(u0 + gs, ulast), lds0 + 4u * (uint32_t)bufsz, wu);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   build(lds, bpl);
-  edge_patch_load(g, pm, min(u0 + gs, ulast), pr);
-  edge_patch_store<512>(g, pr, lds + bufsz, tid);
   floatx4v ob[2][NTW];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -356,9 +390,9 @@ __global__ void __launch_bounds__(512, 1)
     // planes(u) and patch(u + gs) are in LDS; every read of plane buffer (it + 1) & 1 and patch
     // buffer it & 1 (the previous iteration's) is done
     __syncthreads();
-    const long long u2 = u + 2 * gs;
-    if (EC_ABL != 2 && EC_ABL != 5) edge_patch_load(g, pm, min(u2, ulast), pr);  // EC_ABL 2: no patch loads
-    if (EC_ABL != 4) build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
+    // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration)
+    edge_patch_dma(g, pm, min(u + 2 * gs, ulast), lds0 + 4u * (uint32_t)((it & 1) * bufsz), wu);
+    build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
     const __bf16* planes = bpl + (it & 1) * NP * EC3_PL;
     floatx4v acc[2][NTW];
 #pragma unroll
@@ -367,7 +401,7 @@ __global__ void __launch_bounds__(512, 1)
       for (int j = 0; j < NTW; ++j) acc[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int sx = 0; sx < EC3_S; ++sx) {
-      if (sx < S && EC_ABL != 3) {  // EC_ABL 3: no MFMAs
+      if (sx < S) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int p = 16 * (mt0 + t) + li;
@@ -391,9 +425,6 @@ __global__ void __launch_bounds__(512, 1)
         }
       }
     }
-    // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration),
-    // before this unit's global stores: waiting for its loads then never waits for them
-    edge_patch_store<512>(g, pr, lds + (it & 1) * bufsz, tid);
     // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li).  The stored values
     // stay in registers of their own (`ob`, live across the unit loop): overwriting a store's data
     // registers waits for the store
@@ -414,11 +445,19 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ox = seg * SEG + 16 * (mt0 + t) + li;
-      if (ox < g.Wo && ((EC_ABL != 1 && EC_ABL != 5) || ob[t][0][0] == 1234.5678f)) {  // EC_ABL 1: (almost) no stores
+      // branch-free: pixels past the row store into a dump slot (no exec-masked memory operation,
+      // so the waitcnt pass counts the stores exactly)
+      float* dst = ox < g.Wo ? yb + (long long)ox * ys_w : edge_store_dump + 48 * t;
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) *(floatx4v*)(yb + (long long)ox * ys_w + 16 * j) = ob[t][j];
-      }
+      for (int j = 0; j < NTW; ++j) *(floatx4v*)(dst + 16 * j) = ob[t][j];
     }
+    // the patch DMA issued at the top of this iteration must have landed before the barrier (the next
+    // iteration builds from it); the 2 NTW output stores issued after it may stay in flight.  vmcnt
+    // counts loads and stores in issue order: with the round-5 register-staged patch the compiler's
+    // wait for the patch loads (vmcnt(0) at the loop's merge) also waited for the previous unit's
+    // 48 KB of output stores (round 6: g_a.0 fwd 0.174 -> 0.170 ms alternating, r09e; the kernel is
+    // bound by its MFMA and store energy rather than by that wait: profiles/r09c_x3d_edge_ablations.txt)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NTW) : "memory");
   }
 }
 

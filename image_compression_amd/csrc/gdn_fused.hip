@@ -53,24 +53,12 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 #ifndef GDN_BWD_DMA_B
 #define GDN_BWD_DMA_B 1  // fused backward: group B issues the next tile's DMA (0: group A, after its first MFMAs)
 #endif
-#ifndef GDN_BWD_X3W
-#define GDN_BWD_X3W 1  // fused split backward: gdn_bwd_x3w_kernel (one wave per SIMD, pipelined)
-#endif
 #ifndef X3W_ABL
 #define X3W_ABL 0  // diagnostic ablations of gdn_bwd_x3w_kernel (wrong results): 1 no loads in the loop, 2 no
                    // phase A, 4 no dgamma MFMAs, 8 no dx MFMAs, 16 no dx stores
 #endif
 #ifndef X3W_STAMP
 #define X3W_STAMP 0  // diagnostic: per-iteration s_memtime stamps of gdn_bwd_x3w_kernel into the workspace
-#endif
-#ifndef GDN_BWD_X3W_BF16
-#define GDN_BWD_X3W_BF16 0  // 1: C3's GDN backward (bf16 operands) on gdn_bwd_x3w_kernel<192, INV, 1> (r07u: 0.341 vs 0.333 ms at 128^2, C3 -1 %); 0: gdn_bwd_fused_kernel
-#endif
-#ifndef X3W_LATE
-#define X3W_LATE 0  // gdn_bwd_x3w_kernel: phase A's last part in the dgamma GEMM's MFMA shadows (r08f: 12-14 VGPRs spilled, 0.49 -> 0.55 ms at 128^2), off
-#endif
-#ifndef X3W_LATE_V
-#define X3W_LATE_V 5  // X3W_LATE: VALU per 32x32x16 MFMA in the dgamma section's schedule
 #endif
 #ifndef X3W_SGB
 #define X3W_SGB 1  // gdn_bwd_x3w_kernel: interleave phase A / epilogue with the MFMAs (sched_group_barrier)
@@ -1112,7 +1100,7 @@ __global__ void __launch_bounds__(256, 1)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[1][j][st], cur[0], acc[j], 0, 0, 0);
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gx[0][j][st], cur[0], acc[j], 0, 0, 0);
           }
-          if (!(X3W_LATE && pr == K32 / 2 - 1)) pa_slice(pr, 3 * h2 + j);
+          pa_slice(pr, 3 * h2 + j);
           if (X3W_SGB) {
 #pragma unroll
             for (int k = 0; k < (NP == 1 ? 1 : 6); ++k) {
@@ -1166,18 +1154,12 @@ __global__ void __launch_bounds__(256, 1)
         }
         acc_s[3 + j][tid] += d;
       }
-      // X3W_LATE: the last part of phase A(t+G) here, two slices per column group, in the free issue
-      // cycles of the 32x32x16 MFMAs (24 of 32 each) instead of the dx GEMM's 16x16x32 shadows (8 of 16)
-      if (X3W_LATE) {
-        pa_slice(K32 / 2 - 1, 2 * j);
-        pa_slice(K32 / 2 - 1, 2 * j + 1);
-      }
       if (X3W_SGB) {
 #pragma unroll
         for (int k = 0; k < (NP == 1 ? 3 : 18); ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
           if (k < 6) __builtin_amdgcn_sched_group_barrier(0x100, NP == 1 ? 2 : 1, 0);  // DS read (the next bb)
-          __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : (X3W_LATE ? X3W_LATE_V : 2), 0);  // VALU
+          __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : 2, 0);  // VALU
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1333,34 +1315,12 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum,
                   void* dxb) {
   float* slab = (float*)ws;
-  if (split == 2 && C == 192 && GDN_BWD_X3W_BF16) {  // bf16 operands (C3) on the pipelined one-wave kernel
-    const int grid = bwd_grid(P);
-    if (grid < 1) return IC_OK;
-    __bf16* b = (__bf16*)dxb;
-    if (inverse && dxb)
-      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, true, 1, true>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma,
-                         dx, slab, (uint32_t)P, b);
-    else if (inverse)
-      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, true, 1>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx,
-                         slab, (uint32_t)P, b);
-    else if (dxb)
-      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, false, 1, true>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma,
-                         dx, slab, (uint32_t)P, b);
-    else
-      hipLaunchKernelGGL((gdn_bwd_x3w_kernel<192, false, 1>), dim3(grid), dim3(256), 0, s, x, norm, dy, gamma, dx,
-                         slab, (uint32_t)P, b);
-    IC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((GDN_SLAB(192) + 63) / 64), dim3(256), 0, s, slab, grid, 192,
-                       dgamma, dbeta, dxsum);
-    IC_CHECK_LAUNCH();
-    return IC_OK;
-  }
   if (split == 2 && C == 192 && dxb)
     return gdn_bwd_fused_launch<192, true, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab,
                                                        s, dxb);
   if (split == 2 && C == 192)
     return gdn_bwd_fused_launch<192, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
-  if (split && C == 192 && GDN_BWD_X3W) {
+  if (split && C == 192) {  // split arithmetic: the pipelined one-wave kernel
     const int grid = bwd_grid(P);
     if (grid < 1) return IC_OK;
     if (inverse)
@@ -1375,8 +1335,6 @@ int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const floa
     IC_CHECK_LAUNCH();
     return IC_OK;
   }
-  if (split && C == 192)
-    return gdn_bwd_fused_launch<192, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
   switch (C) {
     case 64: return gdn_bwd_fused_launch<64>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);
     case 128: return gdn_bwd_fused_launch<128>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab, s);

@@ -770,16 +770,6 @@ __global__ void __launch_bounds__(64 * (BM / WM) * (BN / WN), (BM == 64 ? 3 : 2)
 #ifndef IG_X3D_DMA_J
 #define IG_X3D_DMA_J 4  // DMA_AT 2: before n-tile j's MFMAs (r03zx-r03zy: j = 4 of 12, 1.7-2.7 % per C2 step over 0)
 #endif
-#ifndef IG_X3D_M32
-#define IG_X3D_M32 0  // v_mfma_f32_32x32x16_bf16 wave tiles (ig_kernel_x3d<true>): 18 % slower on g_a.2 fwd (r08a), off
-#endif
-#ifndef IG_X3D_DMA_J32
-#define IG_X3D_DMA_J32 2  // M32: the next chunk's DMA issues before column tile j's MFMAs (of 6)
-#endif
-#ifndef IG_X3D_ABL
-#define IG_X3D_ABL 0  // diagnostic ablations of ig_kernel_x3d<false> (wrong results): 1 = no A split, 2 = no DMA, 3 = no wait for
-                      // the DMA, 4 = no B DMA, 5 = no A DMA
-#endif
 #ifndef IG_X3D_MINT
 #define IG_X3D_MINT 32  // smaller grids: 256-row tiles with K split to fill the chip (>= this many tiles)
 #endif
@@ -800,15 +790,9 @@ __device__ __forceinline__ void ig_glds16(const void* src, uint32_t lds) {
 
 __device__ __forceinline__ int ig_swa(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
 
-// M32: v_mfma_f32_32x32x16_bf16 on 32 x 192 wave tiles (one 32-row tile, six 32-column tiles, two
-// K steps of 16 per chunk): half the MFMA issues of the 16x16x32 form for the same products, and
-// an MFMA holds the SIMD's vector issue for 8 of its 32 cycles instead of 8 of 16, so the A split's
-// VALU has 1.5x the free issue cycles per FLOP (MI355X_MICROARCH.md).  Same operands, LDS images,
-// DMA and chunk order; the MFMA's internal K-sum is 16 instead of 32, so not bitwise the 16x16 form.
-template <bool M32>
 __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
-  constexpr int BM = 256, BN = 192, WM = M32 ? 32 : IG_X3D_WM, WN = BM * BN / 8 / WM, LDB = 32;
-  constexpr int TM = WM / (M32 ? 32 : 16), TN = WN / (M32 ? 32 : 16);
+  constexpr int BM = 256, BN = 192, WM = IG_X3D_WM, WN = BM * BN / 8 / WM, LDB = 32;
+  constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
   constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
   constexpr int STAGE = ASTAGE + BSTAGE;
@@ -867,13 +851,11 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   }
   const float* __restrict__ xg = d.x;
   auto issue = [&](int cc, int t, int st) {
-    if (IG_X3D_ABL == 2) return;  // diagnostic: no DMA
     const uint32_t sb = lbase + (uint32_t)(st * STAGE);
     const int dy = P.dy[t], dx = P.dx[t];
     const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (IG_X3D_ABL == 5) break;  // diagnostic: no A DMA
       const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
       const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
       ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
@@ -882,7 +864,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 32);
 #pragma unroll
     for (int kb = 0; kb < 5; ++kb) {
-      if (IG_X3D_ABL == 4) break;  // diagnostic: no B DMA
       if (w + 8 * kb < NB) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (w + 8 * kb) * 1024));
     }
   };
@@ -892,65 +873,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
   if (cb < ce) {
     issue(cn, tn, 0);
     if (++tn == T) { tn = 0; ++cn; }
-  }
-  if constexpr (M32) {
-    // 32x32x16 fragments: lane holds row / column lane & 31, K values 16 ks + 8 h .. + 8 (h = lane >> 5)
-    const int r = lane & 31, h = lane >> 5;
-    int ach[2][2], bch[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      ach[ks][0] = ((4 * ks + 2 * h) ^ ig_swa(r & 15)) << 2;
-      ach[ks][1] = ((4 * ks + 2 * h + 1) ^ ig_swa(r & 15)) << 2;
-      bch[ks] = 8 * ((2 * ks + h) ^ ig_swz(r));
-    }
-    floatx16 acc[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    for (int c = cb; c < ce; ++c) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
-      const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
-      bf16x8 a[3][2];
-      const float* ar = As + (wm * WM + r) * 32;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const floatx4v lo = *(const floatx4v*)(ar + ach[ks][0]);
-        const floatx4v hi = *(const floatx4v*)(ar + ach[ks][1]);
-        bf16x4 h0, m0v, l0, h1, m1v, l1;
-        split3_bf16x4(lo, h0, m0v, l0);
-        split3_bf16x4(hi, h1, m1v, l1);
-        a[0][ks] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-        a[1][ks] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
-        a[2][ks] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if (j == IG_X3D_DMA_J32 && c + 1 < ce) {
-          issue(cn, tn, (c + 1 - cb) & 1);
-          if (++tn == T) { tn = 0; ++cn; }
-        }
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          bf16x8 b[3];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 32 + r) * LDB + bch[ks]);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][ks], b[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[2], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][ks], b[0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][ks], b[0], acc[j], 0, 0, 0);
-        }
-      }
-    }
-    floatx16 acc2[1][TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc2[0][j] = acc[j];
-    ig_epilogue<1, TN>(d, P, acc2, M, m0, 0, wm, wn, WM, WN, r, h, split);
-    return;
   }
   const int r = lane & 15, g = lane >> 4;
   const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
@@ -962,7 +884,7 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 
   for (int c = cb; c < ce; ++c) {
-    if (IG_X3D_ABL != 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ABL 3: diagnostic, no wait
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
     const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
@@ -977,17 +899,8 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
       const floatx4v lo = *(const floatx4v*)(ar + ach0);
       const floatx4v hi = *(const floatx4v*)(ar + ach1);
       bf16x4 h0, m0v, l0, h1, m1v, l1;
-#if IG_X3D_ABL == 1
-      // diagnostic (wrong results): one conversion per value instead of the split
-      {
-        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-        h0 = m0v = l0 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3])});
-        h1 = m1v = l1 = __builtin_bit_cast(bf16x4, u32x2{ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
-      }
-#else
       split3_bf16x4(lo, h0, m0v, l0);
       split3_bf16x4(hi, h1, m1v, l1);
-#endif
       a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
       a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
       a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -1015,156 +928,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_x3d(const IgDesc d) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
       }
-    }
-  }
-  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
-}
-
-// ig_kernel_x3d with the LDS-DMA on producer waves (IG_X3D_PC): 12 waves, the 8 consumer waves only
-// read fragments, split A and run the MFMAs (x3d's wave tiles and order: bitwise its result), and one
-// producer wave per SIMD issues all 68 DMA pieces of the next chunk (17 each) right after the chunk's
-// barrier and waits for them before the next.  An LDS-DMA piece costs its issuing wave 60-185 cycles
-// (MI355X_MICROARCH.md), 8.5 pieces per chunk on each MFMA wave in x3d; here no MFMA wave issues one.
-// Three waves per SIMD: the consumers must fit 168 registers (x3d's waves hold 217 with the DMA
-// addresses).
-#ifndef IG_X3D_PC
-#define IG_X3D_PC 0  // measured 5 % slower per C2 step than ig_kernel_x3d (r08g), off
-#endif
-__global__ void __launch_bounds__(768, 1) ig_kernel_x3pc(const IgDesc d) {
-  constexpr int BM = 256, BN = 192, WM = 32, WN = 192, LDB = 32;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ASTAGE = BM * 32 * 4;       // bytes of the fp32 A image (32 KB)
-  constexpr int BSTAGE = 3 * BN * LDB * 2;  // bytes of the three bf16 B planes (36 KB)
-  constexpr int STAGE = ASTAGE + BSTAGE;
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
-
-  const int zi = blockIdx.z;
-  const int phase = zi / d.ksplit;
-  const int split = zi - phase * d.ksplit;
-  const IgPhase& P = d.ph[phase];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  const int T = P.T;
-  const int nchunks = T * (d.Cin >> 5);
-  const int cb = split * d.kcps;
-  const int ce = min(nchunks, cb + d.kcps);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-  if (w >= 8) {
-    // ---------------------------------------------------------------- producer waves
-    const int pw = w - 8;
-    const uint32_t lbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
-    // A: producer pw DMAs pieces 8 pw + k (k < 8), rows 8 (8 pw + k) + (lane >> 3); lane's physical
-    // chunk lane & 7 holds logical chunk (lane & 7) ^ ig_swa(row)
-    const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
-    uint32_t a_off[8];
-    int a_iy[8], a_ix[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int row = 64 * pw + 8 * k + (lane >> 3);
-      const uint32_t m = m0 + row;
-      const bool ok = m < M;
-      const uint32_t mm = ok ? m : 0u;
-      const uint32_t img = fdiv(mm, P.fd_hw);
-      const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
-      const uint32_t gy = fdiv(rem, P.fd_w);
-      const uint32_t gx = rem - gy * (uint32_t)P.Wg;
-      a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
-      a_ix[k] = (int)gx * d.stride;
-      a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
-                 4u * (uint32_t)((lane & 7) ^ ig_swa(row & 15));
-    }
-    // B: producer pw DMAs pieces jj = pw + 4 kb (kb < 9): plane jj / 12, rows 16 (jj % 12) + (lane >> 2)
-    const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-    uint32_t b_off[9];
-#pragma unroll
-    for (int kb = 0; kb < 9; ++kb) {
-      const int jj = pw + 4 * kb;
-      const int q = jj / 12, rb = 16 * (jj - 12 * q) + (lane >> 2);
-      b_off[kb] = (uint32_t)q * (uint32_t)d.wplane + (uint32_t)rb * (uint32_t)d.Cin +
-                  8u * (uint32_t)((lane & 3) ^ ig_swz(rb));
-    }
-    const float* __restrict__ xg = d.x;
-    auto issue = [&](int cc, int t, int st) {
-      const uint32_t sb = lbase + (uint32_t)(st * STAGE);
-      const int dy = P.dy[t], dx = P.dx[t];
-      const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + cc * 32);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
-        const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
-        ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
-                  sb + (uint32_t)((8 * pw + k) * 1024));
-      }
-      const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + cc * 32);
-#pragma unroll
-      for (int kb = 0; kb < 9; ++kb) ig_glds16(wpb + (b_off[kb] + boff), sb + (uint32_t)(ASTAGE + (pw + 4 * kb) * 1024));
-    };
-    int cn = cb / T, tn = cb - (cb / T) * T;
-    if (cb < ce) {
-      issue(cn, tn, 0);
-      if (++tn == T) { tn = 0; ++cn; }
-    }
-    for (int c = cb; c < ce; ++c) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // chunk c published; stage (c + 1) & 1 free (chunk c - 1 done)
-      if (c + 1 < ce) {
-        issue(cn, tn, (c + 1 - cb) & 1);
-        if (++tn == T) { tn = 0; ++cn; }
-      }
-    }
-    return;
-  }
-
-  // ------------------------------------------------------------------ consumer waves (x3d's loop)
-  const int wm = w, wn = 0;
-  const int r = lane & 15, g = lane >> 4;
-  const int ach0 = ((2 * g) ^ ig_swa(r)) << 2, ach1 = ((2 * g + 1) ^ ig_swa(r)) << 2;
-  const int bch = 8 * (g ^ ig_swz(r));
-  floatx4v acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-  for (int c = cb; c < ce; ++c) {
-    __syncthreads();
-    const float* As = (const float*)(lds + ((c - cb) & 1) * STAGE);
-    const __bf16* Bs = (const __bf16*)(lds + ((c - cb) & 1) * STAGE + ASTAGE);
-    bf16x8 a[3][TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* ar = As + (wm * WM + i * 16 + r) * 32;
-      const floatx4v lo = *(const floatx4v*)(ar + ach0);
-      const floatx4v hi = *(const floatx4v*)(ar + ach1);
-      bf16x4 h0, m0v, l0, h1, m1v, l1;
-      split3_bf16x4(lo, h0, m0v, l0);
-      split3_bf16x4(hi, h1, m1v, l1);
-      a[0][i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[1][i] = __builtin_shufflevector(m0v, m1v, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[2][i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bf16x8 b[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) b[q] = *(const bf16x8*)(Bs + (q * BN + wn * WN + j * 16 + r) * LDB + bch);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
-      }
-      // at most the next column tile's B fragments ahead: 168 registers hold 96 accumulators, the
-      // split A fragments and two B fragment sets, not all twelve
-      __builtin_amdgcn_sched_barrier(0);
     }
   }
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
@@ -1300,145 +1063,6 @@ __global__ void __launch_bounds__(512, 1) ig_kernel_b16d(const IgDesc d) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b1, acc[i][j], 0, 0, 0);
       }
     }
-  }
-  ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
-}
-
-// ig_kernel_b16d's tiles, waves and MFMA order on a ring of S 32-channel slots (A 16 KB + B 12 KB each,
-// 140 KB at S = 5) instead of two 64-channel stages: each chunk's LDS-DMA issues S - 1 chunks ahead of
-// its MFMAs and the wait before a chunk's barrier (s_waitcnt vmcnt(n)) leaves the later chunks in
-// flight.  A two-stage chunk had about 0.7 us of MFMAs per SIMD to hide the DMA issued a third of the
-// way into it (C3's wg_x3p showed the same load latency, r07z).  Chunk c32 runs tap (c32 / 2) % T,
-// channels 64 (c32 / 2T) + 32 (c32 & 1): the MFMAs of every accumulator in b16d's order, so the result
-// is bitwise that kernel's (the plan's chunk ranges stay in 64-channel units).  Rows of 64 B, 16-B
-// pieces XOR ig_swz(row) (as ig_kernel_x3d's B planes): conflict-free ds_read_b128 fragments.
-#ifndef IG_B16R
-#define IG_B16R 0  // measured 21 % slower than ig_kernel_b16d on C3 (r08b: twice the barriers per MFMA), off
-#endif
-#ifndef IG_B16R_S
-#define IG_B16R_S 5
-#endif
-#ifndef IG_B16R_DMA_J
-#define IG_B16R_DMA_J 2  // the DMA of chunk c + S - 1 issues before column tile j's MFMAs of chunk c
-#endif
-// s_waitcnt vmcnt(n), n a wave-uniform multiple of 3 or 4 up to 4 (S - 2)
-__device__ __forceinline__ void ig_wait_vm(int n) {
-  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-__global__ void __launch_bounds__(512, 1) ig_kernel_b16r(const IgDesc d) {
-  constexpr int BM = 256, BN = 192, WM = 32, WN = 192, TM = WM / 16, TN = WN / 16, S = IG_B16R_S;
-  static_assert(S >= 2 && S <= 5, "4 (S - 2) outstanding pieces at most 12");
-  constexpr int ASTAGE = BM * 64;  // 16 KB: 256 rows x 32 bf16
-  constexpr int BSTAGE = BN * 64;  // 12 KB: 192 rows x 32 bf16
-  constexpr int STAGE = ASTAGE + BSTAGE;
-  __shared__ __attribute__((aligned(16))) char lds[S * STAGE];
-
-  const int zi = blockIdx.z;
-  const int phase = zi / d.ksplit;
-  const int split = zi - phase * d.ksplit;
-  const IgPhase& P = d.ph[phase];
-  uint32_t bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  if ((int)bx >= P.mtiles) return;
-  const uint32_t M = (uint32_t)d.N * P.fd_hw.d;
-  const uint32_t m0 = bx * BM;
-  const int T = P.T;
-  const int nchunks = T * (d.Cin >> 6);  // 64-channel units, as the plan's kcps
-  const int cb = 2 * (split * d.kcps);
-  const int ce = 2 * min(nchunks, split * d.kcps + d.kcps);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t lbase = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
-
-  // A: wave w DMAs rows 32w + 16k + (lane >> 2), k < 2 (1 KB = 16 rows of 64 B per piece); lane's
-  // physical piece lane & 3 holds logical piece (lane & 3) ^ ig_swz(row)
-  const uint32_t xsh = (uint32_t)d.xs_h, xsw = (uint32_t)d.xs_w;
-  uint32_t a_off[2];
-  int a_iy[2], a_ix[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int row = 32 * w + 16 * k + (lane >> 2);
-    const uint32_t m = m0 + row;
-    const bool ok = m < M;
-    const uint32_t mm = ok ? m : 0u;
-    const uint32_t img = fdiv(mm, P.fd_hw);
-    const uint32_t rem = mm - img * (uint32_t)P.fd_hw.d;
-    const uint32_t gy = fdiv(rem, P.fd_w);
-    const uint32_t gx = rem - gy * (uint32_t)P.Wg;
-    a_iy[k] = ok ? (int)gy * d.stride : -0x40000000;
-    a_ix[k] = (int)gx * d.stride;
-    a_off[k] = img * (uint32_t)d.xs_n + (uint32_t)a_iy[k] * xsh + (uint32_t)a_ix[k] * xsw +
-               8u * (uint32_t)((lane & 3) ^ ig_swz(row));
-  }
-  // B: 12 pieces of 16 rows; wave w DMAs piece w, and waves 0-3 piece 8 + w too
-  const int nbp = w < 4 ? 2 : 1;
-  const int pw = 2 + nbp;  // DMA pieces per chunk of this wave
-  const __bf16* __restrict__ wpb = (const __bf16*)P.wp;
-  uint32_t b_off[2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int rb = 16 * (w + 8 * kb) + (lane >> 2);
-    b_off[kb] = (uint32_t)rb * (uint32_t)d.Cin + 8u * (uint32_t)((lane & 3) ^ ig_swz(rb));
-  }
-  const __bf16* __restrict__ xg = (const __bf16*)d.xb;
-  const int T2 = 2 * T;
-  auto issue = [&](int c, int slot) {
-    const int cn = c / T2, rm = c - cn * T2, t = rm >> 1;
-    const int c32 = 2 * cn + (rm & 1);  // 32-channel block
-    const uint32_t sb = lbase + (uint32_t)(slot * STAGE);
-    const int dy = P.dy[t], dx = P.dx[t];
-    const uint32_t toff = (uint32_t)(dy * (int)xsh + dx * (int)xsw + c32 * 32);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int iy = a_iy[k] + dy, ix = a_ix[k] + dx;
-      const bool in = (unsigned)iy < (unsigned)d.Hx && (unsigned)ix < (unsigned)d.Wx;
-      ig_glds16(in ? (const void*)(xg + (a_off[k] + toff)) : (const void*)ig_zero_page,
-                sb + (uint32_t)((2 * w + k) * 1024));
-    }
-    const uint32_t boff = (uint32_t)(t * d.Npad * d.Cin + c32 * 32);
-    ig_glds16(wpb + (b_off[0] + boff), sb + (uint32_t)(ASTAGE + w * 1024));
-    if (nbp == 2) ig_glds16(wpb + (b_off[1] + boff), sb + (uint32_t)(ASTAGE + (8 + w) * 1024));
-  };
-
-  const int wm = w, wn = 0;
-  const int r = lane & 15, g = lane >> 4;
-  const int ch = 16 * (g ^ ig_swz(r));
-  floatx4v acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int k = 0; k < S - 1; ++k)
-    if (cb + k < ce) issue(cb + k, k);
-  int slot = 0, islot = S - 1;  // slot of chunk c; slot chunk c + S - 1 goes to
-  for (int c = cb; c < ce; ++c) {
-    // chunk c's pieces landed; the ones of chunks c + 1 .. c + S - 2 may stay in flight
-    ig_wait_vm((min(ce - 1, c + S - 2) - c) * pw);
-    __syncthreads();
-    const char* As = lds + slot * STAGE;
-    const char* Bs = As + ASTAGE;
-    bf16x8 a[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = *(const bf16x8*)(As + (wm * WM + i * 16 + r) * 64 + ch);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (j == IG_B16R_DMA_J && c + S - 1 < ce) issue(c + S - 1, islot);  // into chunk c - 1's slot
-      const bf16x8 b = *(const bf16x8*)(Bs + (wn * WN + j * 16 + r) * 64 + ch);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
-    }
-    slot = slot == S - 1 ? 0 : slot + 1;
-    islot = islot == S - 1 ? 0 : islot + 1;
   }
   ig_epilogue16<TM, TN>(d, P, acc, M, m0, 0, wm, wn, WM, WN, lane, split);
 }
@@ -1638,17 +1262,9 @@ int ig_run(IgDesc& d, hipStream_t s) {
     if (d.bm != 256 || d.Npad != 192 || d.a_op != AOP_NONE) return IC_ERR_ARG;
     if (d.bf16) {
       if (!d.xb || d.Cin % 64 != 0) return IC_ERR_ARG;
-      if (IG_B16R)
-        hipLaunchKernelGGL(ig_kernel_b16r, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
-      else
-        hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      hipLaunchKernelGGL(ig_kernel_b16d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     } else {
-      if (IG_X3D_PC)
-        hipLaunchKernelGGL(ig_kernel_x3pc, dim3(mt, 1, d.nphase * d.ksplit), dim3(768), 0, s, d);
-      else if (IG_X3D_M32)
-        hipLaunchKernelGGL(ig_kernel_x3d<true>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
-      else
-        hipLaunchKernelGGL(ig_kernel_x3d<false>, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
+      hipLaunchKernelGGL(ig_kernel_x3d, dim3(mt, 1, d.nphase * d.ksplit), dim3(512), 0, s, d);
     }
     IC_CHECK_LAUNCH();
     rc = IC_OK;

@@ -726,13 +726,7 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #define WG_X3_DUAL 1
 #endif
 #ifndef WG_X3G
-#define WG_X3G 1  // 5x5 stride-2 192x192 weight gradients on the tap-group kernel (wg_x3g_kernel); 0: wg_x3d_kernel
-#endif
-#ifndef WG_X3G_ABL
-#define WG_X3G_ABL 0  // diagnostic ablations of wg_x3g_kernel (wrong results): 1 no G staging, 2 no X staging, 4 no MFMAs
-#endif
-#ifndef WG_X3P
-#define WG_X3P 1  // the tap-group weight gradients on producer / consumer waves (wg_x3p_kernel); 0: wg_x3g_kernel
+#define WG_X3G 1  // 5x5 stride-2 192x192 weight gradients on the tap-group kernel (wg_x3p_kernel); 0: wg_x3d_kernel
 #endif
 #ifndef WG_X3P_DEEP  // bf16-copy producers keep three steps of loads in flight instead of two
 #define WG_X3P_DEEP 1
@@ -983,223 +977,16 @@ __global__ void __launch_bounds__(512, 1) wg_x3d_kernel(const WgDesc d) {
 // down.  Against wg_x3d_kernel (one tap per block) the staged bytes, the split work and the LDS
 // writes per step fall by a third; the MFMAs, their order and the accumulation order per output
 // element are the same, so the result is bitwise that kernel's.  Two groups run in one launch
-// (the body is instantiated for NTAP = 3 and 2); 25 blocks per split, as before.
-template <bool XSQ, int NTAP, int NP>
-__device__ __forceinline__ void wg_x3g_body(const WgDesc& d, __bf16* lds, int split, int ky, int ct) {
-  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-  constexpr int CW = 192 / NTAP;          // X channels per block
-  constexpr int BM = 192, WM = 96, WN = 48, BK = 32;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int PITCH = 192;
-  constexpr int XR = BK + NTAP - 1;       // X pixel rows per step
-  constexpr int GPLANE = BK * PITCH, XPLANE = 34 * PITCH;
-  constexpr int GOPER = NP * GPLANE;
-  constexpr int STAGE = NP * (GPLANE + XPLANE);
-  constexpr int NT = 512;
-  constexpr int QG = BK * (BM / 4) / NT;  // 3 float4 of G per thread
-  constexpr int XQ4 = XR * (CW / 4);      // float4 of X per step
-  constexpr int QX = (XQ4 + NT - 1) / NT; // 2
-  static_assert(QG * NT == BK * BM / 4 && 2 * QG == TM && QX <= QG, "staged slots per row-tile pair");
-  const int kx0 = NTAP == 3 ? 0 : 1;
-  const int t0 = ky * 5 + kx0;
-  const int c0 = ct * CW;
-  const int pb = split * d.pps;
-  int pe = pb + d.pps;
-  if (pe > (int)d.P) pe = (int)d.P;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int dyt = d.dy[t0], dx0 = d.dx[t0];
-
-  auto swz = [](int row) { return ((((row >> 1) & 1) << 5) | (((row >> 3) & 1) << 4)); };
-  int grow[QG], gcol[QG], xrow[QX], xcol[QX];
-#pragma unroll
-  for (int q = 0; q < QG; ++q) {
-    const int f = tid + NT * q;
-    grow[q] = f / (BM / 4);
-    gcol[q] = (f - grow[q] * (BM / 4)) * 4;
-  }
-#pragma unroll
-  for (int q = 0; q < QX; ++q) {
-    const int f = min(tid + NT * q, XQ4 - 1);  // past the image: a second copy of the last float4
-    xrow[q] = f / (CW / 4);
-    xcol[q] = (f - xrow[q] * (CW / 4)) * 4;
-  }
-  floatx4v gr0[QG], gr1[QG], xr0[QX], xr1[QX];
-  struct StepBase {
-    const float* gb;
-    const float* xb;
-    int gx0;
-    bool rowok, live;
-  };
-  auto step_base = [&](int p0, bool live) {
-    const uint32_t img = fdiv((uint32_t)p0, d.fd_hw);
-    const uint32_t rr = (uint32_t)p0 - img * d.fd_hw.d;
-    const uint32_t gy = fdiv(rr, d.fd_w);
-    const uint32_t gx0 = rr - gy * d.fd_w.d;
-    const int iy = (int)gy * 2 + dyt;
-    return StepBase{d.g + (long long)img * d.gs_n + (long long)gy * d.gs_h + (long long)gx0 * d.gs_w,
-                    d.x + (long long)img * d.xs_n + (long long)iy * d.xs_h, (int)gx0,
-                    live && (unsigned)iy < (unsigned)d.Hx, live};
-  };
-  // branch-free: padding, out-of-range columns and dead steps read a zero page
-  auto gload_q = [&](const StepBase& sb, int q, floatx4v (&rg)[QG], floatx4v (&rx)[QX]) {
-    const float* gs = sb.live ? sb.gb + (long long)grow[q] * d.gs_w + gcol[q] : wg_zero_page;
-    if (!(WG_X3G_ABL & 1)) rg[q] = *(const floatx4v*)gs;
-    if (q < QX && !(WG_X3G_ABL & 2)) {
-      const int ix = (sb.gx0 + xrow[q]) * 2 + dx0;
-      const float* xs = (sb.rowok && (unsigned)ix < (unsigned)d.Wx) ? sb.xb + (long long)ix * d.xs_w + c0 + xcol[q]
-                                                                     : wg_zero_page;
-      floatx4v vx = *(const floatx4v*)xs;
-      if (XSQ) vx = vx * vx;
-      rx[q] = vx;
-    }
-  };
-  auto gload = [&](int p0, floatx4v (&rg)[QG], floatx4v (&rx)[QX], bool live) {
-    const StepBase sb = step_base(p0, live);
-#pragma unroll
-    for (int q = 0; q < QG; ++q) gload_q(sb, q, rg, rx);
-  };
-  auto put = [&](__bf16* dst, int plane, const floatx4v& v) {
-    if constexpr (NP == 1) {
-      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      *(b4*)dst = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
-    } else {
-      b4 vh, vm, vl;
-      split3_bf16x4(v, vh, vm, vl);
-      *(b4*)dst = vh;
-      *(b4*)(dst + plane) = vm;
-      *(b4*)(dst + 2 * plane) = vl;
-    }
-  };
-  auto sstore_q = [&](int buf, int q, const floatx4v (&rg)[QG], const floatx4v (&rx)[QX]) {
-    __bf16* base = lds + buf * STAGE;
-    if (!(WG_X3G_ABL & 1)) put(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q])), GPLANE, rg[q]);
-    if (q < QX && !(WG_X3G_ABL & 2)) put(base + GOPER + xrow[q] * PITCH + (xcol[q] ^ swz(xrow[q])), XPLANE, rx[q]);
-  };
-  auto sstore = [&](int buf, const floatx4v (&rg)[QG], const floatx4v (&rx)[QX]) {
-#pragma unroll
-    for (int q = 0; q < QG; ++q) sstore_q(buf, q, rg, rx);
-  };
-
-  const int wm = w >> 2, wn = w & 3;
-  const int li = lane & 15, lq = lane >> 4;
-  const int tr_r = 8 * lq + (li >> 2);
-  const int tr_c = 4 * (li & 3);
-  floatx4v acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
-
-  // G (A operand): rows tr_r and tr_r + 4 share row bits 1 and 3, so one swizzle serves both reads
-  const int tr_sw = swz(tr_r);
-  auto tr8a = [&](const __bf16* plane, int col) {
-    const __bf16* src = plane + tr_r * PITCH + ((col + tr_c) ^ tr_sw);
-    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)src);
-    const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(src + 4 * PITCH));
-    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  // X (B operand) of column tile j: tap tt's rows are tr_r + tt (and + 4), each with its own swizzle
-  int xo_lo[TN], xo_hi[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int vcol = wn * WN + 16 * j;
-    const int tt = vcol / CW, cc = vcol - (vcol / CW) * CW;
-    const int r0 = tr_r + tt;
-    xo_lo[j] = r0 * PITCH + ((cc + tr_c) ^ swz(r0));
-    xo_hi[j] = (r0 + 4) * PITCH + ((cc + tr_c) ^ swz(r0 + 4));
-  }
-  auto tr8b = [&](const __bf16* plane, int j) {
-    const b4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + xo_lo[j]));
-    const b4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) b4*)(plane + xo_hi[j]));
-    return (b8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  auto step = [&](int p0, int buf, floatx4v (&rg)[QG], floatx4v (&rx)[QX]) {
-    const __bf16* sb = lds + buf * STAGE;
-    b8 bb[NP][TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < NP; ++q) bb[q][j] = tr8b(sb + GOPER + q * XPLANE, j);
-    const int pn = p0 + 3 * BK;
-    const StepBase nb = step_base(pn, pn < pe);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      b8 a[NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) a[q] = tr8a(sb + q * GPLANE, wm * WM + 16 * i);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        floatx4v& c = acc[i][j];
-        if constexpr (NP == 1) {
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
-        } else if (!(WG_X3G_ABL & 4)) {
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bb[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[1][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[2][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bb[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[1][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bb[0][j], c, 0, 0, 0);
-        }
-      }
-      if (i & 1) {
-        // the next step's split + store of slot i / 2, then its refill three steps ahead
-        sstore_q(buf ^ 1, i >> 1, rg, rx);
-        gload_q(nb, i >> 1, rg, rx);
-      }
-    }
-    __syncthreads();
-  };
-
-  const int nsteps = pe > pb ? (pe - pb) / BK : 0;
-  const int q0 = pb - ((nsteps & 1) ? BK : 0);
-  if (nsteps > 0) {
-    if (nsteps & 1) {
-#pragma unroll
-      for (int q = 0; q < QG; ++q) gr0[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < QX; ++q) xr0[q] = floatx4v{0.f, 0.f, 0.f, 0.f};
-    } else {
-      gload(q0, gr0, xr0, true);
-    }
-    sstore(0, gr0, xr0);
-    gload(q0 + BK, gr1, xr1, q0 + BK < pe);
-    gload(q0 + 2 * BK, gr0, xr0, q0 + 2 * BK < pe);
-  }
-  __syncthreads();
-  for (int p0 = q0; p0 < pe; p0 += 2 * BK) {
-    step(p0, 0, gr1, xr1);
-    step(p0 + BK, 1, gr0, xr0);
-  }
-
-  // C/D map of the 16x16 MFMA: row (g) = 4 lq + r, col = li; column tile j belongs to tap tt
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int vcol = wn * WN + 16 * j;
-    const int tt = vcol / CW, cc = vcol - (vcol / CW) * CW;
-    float* slab = d.partial + ((long long)split * d.T + t0 + 2 * tt) * (long long)d.Cg * d.ncols;
-    const int col = c0 + cc + li;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = wm * WM + 16 * i + 4 * lq + r;
-        slab[(long long)gr * d.ncols + col] = acc[i][j][r];
-      }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-}
-
-// Producer / consumer tap groups (WG_X3P, round 5): wg_x3g_body's tiles, LDS images, MFMAs and their
-// order (so bitwise its result), with the staging moved off the MFMA waves.  Twelve waves, three per
+// (the body is instantiated for NTAP = 3 and 2); 25 blocks per split, as before.  Round 4 ran this
+// tiling with the staging inside the MFMA waves (wg_x3g_kernel, removed in round 6: 1.165 ms against
+// wg_x3p's 1.107 on g_a.2, DESIGN_HISTORY.md).
+// Producer / consumer tap groups (round 5): the tap-group tiles, LDS images, MFMAs and their
+// order (bitwise wg_x3d_kernel's result), with the staging moved off the MFMA waves.  Twelve waves, three per
 // SIMD: the eight consumer waves only read fragments and run the MFMAs of step s from one LDS stage;
 // the four producer waves (one per SIMD) meanwhile split and store step s + 1 into the other stage
 // and load step s + 3 into the register set it frees (two sets, loads two steps ahead).  One barrier
 // per step for all twelve.  In wg_x3g the split + store of the next step sat in each MFMA wave's
-// instruction stream (0.36 ms of a 1.19 ms g_a.2 wgrad: WG_X3G_ABL, profiles/r06k_*); a producer wave
+// instruction stream (0.36 ms of a 1.19 ms g_a.2 wgrad: the round-4 kernel's ablations, profiles/r06k_*); a producer wave
 // issues its VALU and LDS stores while its SIMD's MFMA pipe is busy with the consumers' work.
 // B16 (with NP = 1, not XSQ): the producers read G and X from their bf16 copies (d.g16, d.x16: 8 B per
 // four values, nothing converted).  The bf16 weight gradient is bound by the producers' loads (no
@@ -1497,20 +1284,6 @@ __global__ void __launch_bounds__(768, 1) wg_x3p_kernel(const WgDesc d) {
   else wg_x3p_body<XSQ, 2, NP, B16>(d, lds, split, ky, u - 3);
 }
 
-template <bool XSQ, int NP = 3>
-__global__ void __launch_bounds__(512, 1) wg_x3g_kernel(const WgDesc d) {
-  constexpr int STAGE = NP * (32 * 192 + 34 * 192);
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
-  const int nblk = 25 * d.nsplit;
-  const int b = blockIdx.x;
-  const int wid = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);  // XCD-grouped; gridDim.x % 8 == 0
-  if (wid >= nblk) return;
-  const int split = wid / 25, rem = wid - (wid / 25) * 25;
-  const int ky = rem / 5, u = rem - (rem / 5) * 5;
-  if (u < 3) wg_x3g_body<XSQ, 3, NP>(d, lds, split, ky, u);
-  else wg_x3g_body<XSQ, 2, NP>(d, lds, split, ky, u - 3);
-}
-
 struct WgRed {
   const float* partial;
   float* out;    // final [g][c][kk] (G == 1) or level-2 partial [G][g][t][c]
@@ -1645,7 +1418,7 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
   const bool sq = d.x_op == AOP_SQUARE;
   dim3 grid((d.mtiles * d.ntiles * d.T * d.nsplit + 7) / 8 * 8);
   constexpr bool TWO = WG_X3_TWO;
-  if (wg_x3g_ok(d) && WG_X3P) {
+  if (wg_x3g_ok(d)) {
     if (WG_X3P_B16 && d.bf16 && !sq && d.g16 && d.x16) {
       hipLaunchKernelGGL((wg_x3p_kernel<false, 1, true>), grid, dim3(768), 0, s, d);
     } else if (d.bf16) {
@@ -1653,12 +1426,6 @@ int wg_x3_launch(const WgDesc& d, hipStream_t s) {
       else hipLaunchKernelGGL((wg_x3p_kernel<false, 1>), grid, dim3(768), 0, s, d);
     } else if (sq) hipLaunchKernelGGL((wg_x3p_kernel<true>), grid, dim3(768), 0, s, d);
     else hipLaunchKernelGGL((wg_x3p_kernel<false>), grid, dim3(768), 0, s, d);
-  } else if (wg_x3g_ok(d)) {
-    if (d.bf16) {
-      if (sq) hipLaunchKernelGGL((wg_x3g_kernel<true, 1>), grid, dim3(512), 0, s, d);
-      else hipLaunchKernelGGL((wg_x3g_kernel<false, 1>), grid, dim3(512), 0, s, d);
-    } else if (sq) hipLaunchKernelGGL((wg_x3g_kernel<true>), grid, dim3(512), 0, s, d);
-    else hipLaunchKernelGGL((wg_x3g_kernel<false>), grid, dim3(512), 0, s, d);
   } else if (WG_X3_DUAL && d.rowfast && d.Wg % 32 == 0 && d.pps % 32 == 0) {
     if (d.bf16) {
       if (sq) hipLaunchKernelGGL((wg_x3d_kernel<true, false, 1>), grid, dim3(512), 0, s, d);
