@@ -111,6 +111,10 @@ SIGNATURES = {
     "ic_gdn_fwd_xb": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_void, c_int, c_void, c_size, c_void]),
     "ic_gdn_bwd_sum_xb": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_void, c_int,
                                   c_void, c_size, c_void]),
+    # norm recomputed by the C3 backward (round 6): include/imgcomp.h ic_gdn_fwd_rn, ic_gdn_bwd_sum_rn
+    "ic_gdn_fwd_rn": (c_int, [_ACT, c_void, c_void, c_int, _ACT, c_void, c_int, c_void, c_size, c_void]),
+    "ic_gdn_bwd_sum_rn": (c_int, [_ACT, c_void, c_void, c_void, c_int, _ACT, c_void, c_void, c_void, c_void, c_int,
+                                  c_void, c_size, c_void]),
     "ic_conv2d_fwd_xb": (c_int, [_ACT, c_void, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_int, c_void, c_size,
                                  c_void]),
     "ic_conv_transpose2d_dgrad_xb": (c_int, [_ACT, c_void, c_void, c_int, c_int, c_int, _ACT, c_int, c_void, c_size,

@@ -77,10 +77,12 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
       x->sn == y->sn && x->sc == y->sc && x->sh == y->sh && x->sw == y->sw &&
       ((uintptr_t)gamma & 15) == 0) {
     const int mode = (math & IC_MATH_BF16) && split && x->c == 192 ? 2 : split ? 1 : 0;
+    if (!norm && mode != 2) return IC_ERR_ARG;  // norm left out: the bf16 kernel only (ic_gdn_fwd_rn)
     int rc = gdn_fwd_fused(x->data, gamma, beta, inverse, y->data, norm, x->c, P, s, mode, mode == 2 ? yb : nullptr);
     if (rc || !yb || mode == 2) return rc;
     return ig_cvt_bf16(y->data, yb, act_numel(y), s);
   }
+  if (!need && !norm) return IC_ERR_ARG;
   IgDesc d = {};
   gemm1x1(d, x, y);
   d.bias = beta;
@@ -110,7 +112,7 @@ int gdn_fwd_impl(const ic_act* x, const float* gamma, const float* beta, int inv
 
 int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
-                 size_t* need, int math = 0, float* dxsum = nullptr, void* dxb = nullptr);
+                 size_t* need, int math = 0, float* dxsum = nullptr, void* dxb = nullptr, const float* beta = nullptr);
 
 // dxb: dx's compact NHWC bf16 copy as well (the fused bf16 kernel writes it; any other path converts)
 int gdn_bwd_impl_xb(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
@@ -122,7 +124,7 @@ int gdn_bwd_impl_xb(const ic_act* x, const float* norm, const float* dy, const f
 
 int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                  const ic_act* dx, float* dgamma, float* dbeta, void* ws, size_t wsb, hipStream_t s,
-                 size_t* need, int math, float* dxsum, void* dxb) {
+                 size_t* need, int math, float* dxsum, void* dxb, const float* beta) {
   const long long n = act_numel(x);
   const long long P = (long long)x->n * x->h * x->w;
   // fused path: x, dx, norm, dy all NHWC-dense with x's strides; its workspace
@@ -132,11 +134,13 @@ int gdn_bwd_impl(const ic_act* x, const float* norm, const float* dy, const floa
       ((uintptr_t)dy & 15) == 0 && x->sn == dx->sn && x->sc == dx->sc && x->sh == dx->sh && x->sw == dx->sw &&
       wsb >= fused_ws) {
     const int mode = (math & IC_MATH_BF16) && x->c == 192 ? 2 : (math & IC_MATH_SPLIT) ? 1 : 0;
+    if (!norm && mode != 2) return IC_ERR_ARG;  // norm recomputed: the bf16 kernel only (ic_gdn_bwd_sum_rn)
     int rc = gdn_bwd_fused(x->data, norm, dy, gamma, inverse, dx->data, dgamma, dbeta, x->c, P, ws, s, mode, dxsum,
-                           mode == 2 ? dxb : nullptr);
+                           mode == 2 ? dxb : nullptr, beta);
     if (rc || !dxb || mode == 2) return rc;
     return ig_cvt_bf16(dx->data, dxb, act_numel(dx), s);
   }
+  if (!need && !norm) return IC_ERR_ARG;  // norm recomputed: the fused bf16 kernel only
   if (dxb && !need) {  // the general path, then the copy
     int rc = gdn_bwd_impl(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, wsb, s, nullptr, math, dxsum, nullptr);
     if (rc) return rc;
@@ -292,6 +296,19 @@ int ic_gdn_bwd_sum_xb(const ic_act* x, const float* norm, const float* dy, const
   if (!dxb) return IC_ERR_ARG;
   return gdn_bwd_impl_xb(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, math,
                          dxsum, dxb);
+}
+
+int ic_gdn_fwd_rn(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, void* yb,
+                  int math, void* ws, size_t ws_bytes, void* stream) {
+  if (yb && !compact_nhwc(y)) return IC_ERR_ARG;
+  return gdn_fwd_impl(x, gamma, beta, inverse, y, nullptr, ws, ws_bytes, (hipStream_t)stream, nullptr, math, yb);
+}
+int ic_gdn_bwd_sum_rn(const ic_act* x, const float* beta, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, void* dxb, int math, void* ws,
+                      size_t ws_bytes, void* stream) {
+  if (!beta || (dxb && !compact_nhwc(dx))) return IC_ERR_ARG;
+  return gdn_bwd_impl(x, nullptr, dy, gamma, inverse, dx, dgamma, dbeta, ws, ws_bytes, (hipStream_t)stream, nullptr,
+                      math, dxsum, dxb, beta);
 }
 
 }  // extern "C"

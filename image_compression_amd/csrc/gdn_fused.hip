@@ -284,7 +284,9 @@ __global__ void __launch_bounds__(256, 2)
 // nearest even, one plane each, one product, fp32 accumulation.
 // YB (with NP = 1, config C3): y also as a compact bf16 copy (yb), the A operand of the next conv's
 // bf16 DMA tiles (ig_kernel_b16d), so that conv reads 2 B per element and converts nothing.
-template <int C, int NP = 3, bool YB = false>
+// NORM = false (with NP = 1, config C3, round 6): norm is not stored -- the backward recomputes it
+// (gdn_bwd_fused_kernel<..., RN>), 4 of the 14 bytes per element this HBM-bound kernel moves.
+template <int C, int NP = 3, bool YB = false, bool NORM = true>
 __global__ void __launch_bounds__(768, 1)
     gdn_fwd_x3s_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                        const float* __restrict__ beta, int inverse, float* __restrict__ y,
@@ -429,7 +431,7 @@ __global__ void __launch_bounds__(768, 1)
         const float yv = inverse ? xv * __builtin_amdgcn_sqrtf(nv) : xv * __builtin_amdgcn_rsqf(nv);
         const size_t o = (size_t)min(m0 + m, P - 1) * C + n;
         y[o] = yv;
-        norm[o] = nv;
+        if constexpr (NORM) norm[o] = nv;
         if constexpr (YB) yb[o] = (__bf16)yv;  // round to nearest even
       }
     put(lds + b2 * TILE, pt);
@@ -463,15 +465,14 @@ __device__ __forceinline__ int pl_off(int m, int n) {
 // X3: also write q and x^2, split into three bf16 terms, as [pixel][channel]
 // planes (sb: q planes then x^2 planes, swizzled by pl_off) for the split GEMMs
 // BF: bf16 operands (config C3): only the first plane, q and x^2 rounded to nearest even
+// one float4 chunk `pos` (lane-linear position in the swizzled images) with its norm values nv
 template <int C, int BM, bool X3 = false, bool BF = false>
-__device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
-                                                uint32_t P, int inverse, int tid, __bf16* sb = nullptr) {
-  constexpr int NCH = BM * C / 4;
-  for (int pos = tid; pos < NCH; pos += 512) {
+__device__ __forceinline__ void gdn_bwd_phase_a_chunk(int pos, const floatx4v nv, const float* xs, float* gs,
+                                                      float* qs, uint32_t m0, uint32_t P, int inverse, __bf16* sb) {
+  {
     const int off = pos * 4;
     const bool valid = m0 + (uint32_t)(pos / (C / 4)) < P;  // rows past P are zero-filled
     const floatx4v xv = *(const floatx4v*)(xs + off);
-    const floatx4v nv = *(const floatx4v*)(ns + off);
     const floatx4v gv = *(const floatx4v*)(gs + off);
     floatx4v qv, dv;
 #pragma unroll
@@ -525,6 +526,14 @@ __device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns
   }
 }
 
+template <int C, int BM, bool X3 = false, bool BF = false>
+__device__ __forceinline__ void gdn_bwd_phase_a(const float* xs, const float* ns, float* gs, float* qs, uint32_t m0,
+                                                uint32_t P, int inverse, int tid, __bf16* sb = nullptr) {
+  constexpr int NCH = BM * C / 4;
+  for (int pos = tid; pos < NCH; pos += 512)
+    gdn_bwd_phase_a_chunk<C, BM, X3, BF>(pos, *(const floatx4v*)(ns + pos * 4), xs, gs, qs, m0, P, inverse, sb);
+}
+
 // Keep a k-step's MFMAs inside that step: IR-level code motion otherwise sinks
 // chains of them to the end of an unrolled loop, which keeps every step's
 // operand fragments live (sched_barrier only constrains the machine
@@ -560,13 +569,80 @@ __device__ __forceinline__ void bar_wait_lgkm() {
 // the quadrant GEMM with one product on single bf16 planes of q and x^2.
 // XB (with BF): dx also as a compact bf16 copy (dxb), the A operand of the previous transposed conv's
 // input gradient on the bf16 DMA tiles (ig_kernel_b16d).
-template <int C, bool X3, bool BF = false, bool XB = false>
+// RN: one wave's share of phase A with the norm formed in registers.  The wave computes norm^T for its
+// n-tiles tl0 .. tl0 + NT - 1 (16 channels each): norm[m][k] = beta[k] + sum_n bf16(gamma[k][n])
+// bf16(x[m][n]^2) with Gamma's rows as the A operand (gfrag(j, s32), see gdn_norm_frags) and x^2 as B,
+// over the six 16x16x32 K steps in order -- gdn_fwd_x3s_kernel<192, 1>'s products and order, so the
+// forward's norm bitwise -- which leaves each lane the norm of 4 consecutive channels k = 16 tl + 4 lq ..
+// of one pixel m = li: exactly one float4 chunk of phase A, which the lane then runs on its chunks
+// (no norm image, no extra barrier).
+template <int C, int BM, int NT, class GF>
+__device__ __forceinline__ void gdn_norm_phase_a(const float* xs, float* gs, float* qs, __bf16* sb, GF gfrag,
+                                                 const float (&bn)[NT][4], int tl0, int li, int lq, uint32_t m0,
+                                                 uint32_t P, int inverse) {
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  floatx4v an[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) an[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s32 = 0; s32 < C / 32; ++s32) {
+    const int c0 = 8 * s32 + 2 * lq;
+    floatx4v lo = *(const floatx4v*)(xs + li * C + ((c0 ^ li) << 2));
+    floatx4v hi = *(const floatx4v*)(xs + li * C + (((c0 + 1) ^ li) << 2));
+    lo = lo * lo;
+    hi = hi * hi;
+    const b8 b = __builtin_bit_cast(b8, u32x4{ic_cvt_pk_bf16(lo[0], lo[1]), ic_cvt_pk_bf16(lo[2], lo[3]),
+                                               ic_cvt_pk_bf16(hi[0], hi[1]), ic_cvt_pk_bf16(hi[2], hi[3])});
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      an[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gfrag(j, s32), b, an[j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int pos = li * (C / 4) + ((4 * (tl0 + j) + lq) ^ li);  // chunk (m = li, k = 16 tl + 4 lq ..)
+    gdn_bwd_phase_a_chunk<C, BM, true, true>(pos, an[j] + floatx4v{bn[j][0], bn[j][1], bn[j][2], bn[j][3]}, xs, gs,
+                                             qs, m0, P, inverse, sb);
+  }
+}
+
+// the bf16 rows of gamma an RN wave holds (A fragments: g[j][s32][e] = bf16(gamma[k = 16 (tl0 + j) + li][32 s32 +
+// 8 lq + e])) and beta of the 4 output channels 16 (tl0 + j) + 4 lq .. each lane's results are
+template <int C, int NT>
+__device__ __forceinline__ void gdn_norm_frags(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                               __bf16 (&g)[NT][C / 32][8], float (&bn)[NT][4], int tl0, int li,
+                                               int lq) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int k = 16 * (tl0 + j) + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bn[j][r] = beta[16 * (tl0 + j) + 4 * lq + r];  // the lane's output channels
+#pragma unroll
+    for (int s32 = 0; s32 < C / 32; ++s32) {
+      const floatx4v g0 = *(const floatx4v*)(gamma + (size_t)k * C + 32 * s32 + 8 * lq);
+      const floatx4v g1 = *(const floatx4v*)(gamma + (size_t)k * C + 32 * s32 + 8 * lq + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[j][s32][e] = (__bf16)(e < 4 ? g0[e] : g1[e - 4]);
+    }
+  }
+}
+
+// RN (with BF, round 6): norm is not read from HBM but recomputed per tile from the staged x, as the
+// forward formed it (bitwise the forward's norm), inside phase A (gdn_norm_phase_a): each wave forms
+// norm^T for its 16-channel n-tiles on the MFMA and runs phase A on the float4 chunks the result leaves in
+// its lanes -- group A's waves two n-tiles each (the 2/3 of phase A they ran before; Gamma's rows as bf16
+// A fragments, one tile's in 24 VGPRs, the other's in LDS), group B's one each from LDS (its 144 dgamma
+// accumulators leave no registers; 48 KB of LDS in all).  No norm image and no extra barrier; the C3 GDN
+// pair moves 10 + 14 bytes per element instead of 14 + 18.
+template <int C, bool X3, bool BF = false, bool XB = false, bool RN = false>
 __global__ void __launch_bounds__(512, 2)
     gdn_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ norm, const float* __restrict__ dy,
                          const float* __restrict__ gamma, int inverse, float* __restrict__ dx,
-                         float* __restrict__ slab, uint32_t P, __bf16* __restrict__ dxb = nullptr) {
+                         float* __restrict__ slab, uint32_t P, __bf16* __restrict__ dxb = nullptr,
+                         const float* __restrict__ beta = nullptr) {
   static_assert(!X3 || C == 192, "split dgamma tiles 192 x 192 as 2 x 2 quadrants of 96");
   static_assert(!BF || X3, "bf16 operands run on the split kernel's layout");
+  static_assert(!RN || BF, "norm recomputed on the bf16 kernel only");
   constexpr int NP = BF ? 1 : 3;  // bf16 planes per operand image
   constexpr int BM = 16;
   constexpr int NTA = 256;       // threads of group A (staging / copy-out)
@@ -576,10 +652,12 @@ __global__ void __launch_bounds__(512, 2)
   constexpr int KU = C / 16;
   constexpr int TILE = BM * C;
   constexpr int NSTORE = BM * C / 4 / NTA;
-  // per buffer: x, norm, dy images; plus the q image
-  __shared__ __attribute__((aligned(16))) float lds[7 * TILE];
+  // per buffer: x, norm (not with RN), dy images; plus the q image
+  constexpr int BUF = RN ? 2 * TILE : 3 * TILE, DYO = RN ? TILE : 2 * TILE;
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + TILE];
   __shared__ __attribute__((aligned(16))) __bf16 sbf[X3 ? 2 * NP * TILE : 8];  // split q / x^2 images
-  float* const qs = lds + 6 * TILE;
+  __shared__ __attribute__((aligned(16))) __bf16 gnrl[RN ? 12 * (C / 32) * 64 * 8 : 8];  // RN: Gamma's rows, 12 n-tiles
+  float* const qs = lds + 2 * BUF;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -591,10 +669,10 @@ __global__ void __launch_bounds__(512, 2)
   constexpr bool DMA_B = GDN_BWD_DMA_B && (X3 || C < 192);
   // x, norm, dy of tile t into buffer b (256 threads; ti = thread index within the group)
   auto stage = [&](uint32_t t, int b, int ti) {
-    float* base = lds + b * 3 * TILE;
+    float* base = lds + b * BUF;
     stage_tile<C, BM, NTA>(x, t * BM, P, base, ti, lane);
-    stage_tile<C, BM, NTA>(norm, t * BM, P, base + TILE, ti, lane);
-    stage_tile<C, BM, NTA>(dy, t * BM, P, base + 2 * TILE, ti, lane);
+    if constexpr (!RN) stage_tile<C, BM, NTA>(norm, t * BM, P, base + TILE, ti, lane);
+    stage_tile<C, BM, NTA>(dy, t * BM, P, base + DYO, ti, lane);
   };
 
   if (w < 4) {
@@ -605,6 +683,18 @@ __global__ void __launch_bounds__(512, 2)
     constexpr int K32 = C / 32;
     float bfr[BF ? 1 : NTW][BF ? 1 : 4 * KU];
     b8 gbf[BF ? NTW : 1][BF ? K32 : 1];
+    // RN: Gamma's rows of n-tiles 2w, 2w + 1 for gdn_norm_phase_a, parked in LDS (this wave's slots in lane
+    // order: conflict-free 16-B reads)
+    float bnr[2][4];
+    __bf16* gnl = gnrl + (size_t)w * 2 * K32 * 64 * 8;
+    if constexpr (RN) {
+      __bf16 g2[2][K32][8];
+      gdn_norm_frags<C, 2>(gamma, beta, g2, bnr, 2 * w, li, lq);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s32 = 0; s32 < K32; ++s32) *(b8*)(gnl + ((j * K32 + s32) * 64 + lane) * 8) = *(const b8*)g2[j][s32];
+    }
     if constexpr (BF) {
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
@@ -632,9 +722,14 @@ __global__ void __launch_bounds__(512, 2)
       __builtin_amdgcn_s_barrier();  // B1
       first = false;
       const uint32_t nxt = tile + gridDim.x;
-      float* xs = lds + buf * 3 * TILE;
-      float* gs = xs + 2 * TILE;  // dy, then the direct term of dx, then dx
-      gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
+      float* xs = lds + buf * BUF;
+      float* gs = xs + DYO;  // dy, then the direct term of dx, then dx
+      if constexpr (RN)
+        gdn_norm_phase_a<C, BM, 2>(xs, gs, qs, sbf,
+                                   [&](int j, int s32) { return *(const b8*)(gnl + ((j * K32 + s32) * 64 + lane) * 8); },
+                                   bnr, 2 * w, li, lq, tile * BM, P, inverse);
+      else
+        gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, gs, qs, tile * BM, P, inverse, tid, sbf);
       bar_wait_lgkm();  // B2
       floatx4v acc[NTW];
 #pragma unroll
@@ -713,15 +808,30 @@ __global__ void __launch_bounds__(512, 2)
     const int t = tid - 256;
     int buf = 0;
     int it = 0;
+    // RN: Gamma's rows of n-tile 8 + (w - 4) (gdn_norm_phase_a), parked in LDS (this wave's slot, lane order;
+    // group B has no registers to spare beside its 144 dgamma accumulators)
+    float bnr[1][4];
+    __bf16* gnl = gnrl + (size_t)(8 + wq) * (C / 32) * 64 * 8;  // after group A's eight tiles
+    if constexpr (RN) {
+      __bf16 gnr[1][C / 32][8];
+      gdn_norm_frags<C, 1>(gamma, beta, gnr, bnr, 8 + wq, li, lq);
+#pragma unroll
+      for (int s32 = 0; s32 < C / 32; ++s32) *(b8*)(gnl + (s32 * 64 + lane) * 8) = *(const b8*)gnr[0][s32];
+    }
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
-      const float* xs = lds + buf * 3 * TILE;
+      const float* xs = lds + buf * BUF;
       const uint32_t m0 = tile * BM;
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
       if (DMA_B && tile + gridDim.x < ntiles) stage(tile + gridDim.x, buf ^ 1, tid - NTA);
-      gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + 2 * TILE, qs, m0, P, inverse, tid, sbf);
+      if constexpr (RN)
+        gdn_norm_phase_a<C, BM, 1>(xs, (float*)xs + DYO, qs, sbf,
+                                   [&](int, int s32) { return *(const b8*)(gnl + (s32 * 64 + lane) * 8); }, bnr, 8 + wq,
+                                   li, lq, m0, P, inverse);
+      else
+        gdn_bwd_phase_a<C, BM, X3, BF>(xs, xs + TILE, (float*)xs + DYO, qs, m0, P, inverse, tid, sbf);
       bar_wait_lgkm();  // B2
       if (t < C) {
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
@@ -753,7 +863,7 @@ __global__ void __launch_bounds__(512, 2)
       }
       bar_wait_lgkm();  // B3
       if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
-        const float* gsd = xs + 2 * TILE;
+        const float* gsd = xs + DYO;
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) dxs += gsd[swz<C>(m, t)];
       }
@@ -787,7 +897,7 @@ __global__ void __launch_bounds__(512, 2)
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B1
-      const float* xs = lds + buf * 3 * TILE;
+      const float* xs = lds + buf * BUF;
       const uint32_t m0 = tile * BM;
       // group B (idle at B3 while group A finishes dx) issues the next tile's DMA; buffer buf^1
       // is free since B1, and this group's wait before the next B1 covers it
@@ -835,7 +945,7 @@ __global__ void __launch_bounds__(512, 2)
       }
       bar_wait_lgkm();  // B3
       if (t < C) {  // column sums of this tile's dx (the producing conv's bias gradient)
-        const float* gsd = xs + 2 * TILE;
+        const float* gsd = xs + DYO;
         const int rows = (P - m0) < (uint32_t)BM ? (int)(P - m0) : BM;
         for (int m = 0; m < rows; ++m) dxs += gsd[swz<C>(m, t)];
       }
@@ -1252,14 +1362,14 @@ int bwd_grid(long long P) {
   return (int)(ntiles < 256 ? ntiles : 256);
 }
 
-template <int C, bool X3 = false, bool BF = false, bool XB = false>
+template <int C, bool X3 = false, bool BF = false, bool XB = false, bool RN = false>
 int gdn_bwd_fused_launch(const float* x, const float* norm, const float* dy, const float* gamma, int inverse,
                          float* dx, float* dgamma, float* dbeta, float* dxsum, long long P, float* slab,
-                         hipStream_t s, void* dxb = nullptr) {
+                         hipStream_t s, void* dxb = nullptr, const float* beta = nullptr) {
   const int grid = bwd_grid(P);
   if (grid < 1) return IC_OK;
-  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3, BF, XB>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma, inverse,
-                     dx, slab, (uint32_t)P, (__bf16*)dxb);
+  hipLaunchKernelGGL((gdn_bwd_fused_kernel<C, X3, BF, XB, RN>), dim3(grid), dim3(512), 0, s, x, norm, dy, gamma,
+                     inverse, dx, slab, (uint32_t)P, (__bf16*)dxb, beta);
   IC_CHECK_LAUNCH();
   const int stride = GDN_SLAB(C);
   hipLaunchKernelGGL(gdn_slab_reduce_kernel, dim3((stride + 63) / 64), dim3(256), 0, s, slab, grid, C, dgamma,
@@ -1282,11 +1392,18 @@ bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long
 
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
                   long long P, hipStream_t s, int split, void* yb) {
+  if (!norm && !(split == 2 && C == 192)) return IC_ERR_ARG;  // only the bf16 kernel can leave norm out
   if (split && C == 192) {  // split: 1 = fp32 by the exact split, 2 = bf16 operands (config C3)
     const long long ntiles = (P + 31) / 32;
     const long long grid = ntiles < 256 ? ntiles : 256;  // one block per CU
     if (grid < 1) return IC_OK;
-    if (split == 2 && yb)
+    if (split == 2 && !norm && yb)  // norm recomputed by the backward (round 6)
+      hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1, true, false>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma,
+                         beta, inverse, y, norm, (uint32_t)P, (__bf16*)yb);
+    else if (split == 2 && !norm)
+      hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1, false, false>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma,
+                         beta, inverse, y, norm, (uint32_t)P);
+    else if (split == 2 && yb)
       hipLaunchKernelGGL((gdn_fwd_x3s_kernel<192, 1, true>), dim3((unsigned)grid), dim3(768), 0, s, x, gamma, beta,
                          inverse, y, norm, (uint32_t)P, (__bf16*)yb);
     else if (split == 2)
@@ -1313,8 +1430,17 @@ size_t gdn_bwd_fused_ws(int C, long long P) {
 
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split, float* dxsum,
-                  void* dxb) {
+                  void* dxb, const float* beta) {
   float* slab = (float*)ws;
+  if (split == 2 && C == 192 && !norm) {  // norm recomputed from x, gamma and beta (round 6)
+    if (!beta) return IC_ERR_ARG;
+    if (dxb)
+      return gdn_bwd_fused_launch<192, true, true, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum,
+                                                               P, slab, s, dxb, beta);
+    return gdn_bwd_fused_launch<192, true, true, false, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P,
+                                                              slab, s, nullptr, beta);
+  }
+  if (!norm) return IC_ERR_ARG;
   if (split == 2 && C == 192 && dxb)
     return gdn_bwd_fused_launch<192, true, true, true>(x, norm, dy, gamma, inverse, dx, dgamma, dbeta, dxsum, P, slab,
                                                        s, dxb);

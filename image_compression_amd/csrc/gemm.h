@@ -161,13 +161,16 @@ bool gdn_fused_ok(const float* x, const float* y, const float* norm, int C, long
                   long long sn, int H, int W, long long P);
 int gdn_fwd_fused(const float* x, const float* gamma, const float* beta, int inverse, float* y, float* norm, int C,
                   long long P, hipStream_t s, int split = 0,  // split: C = 192 in split arithmetic
-                  void* yb = nullptr);                         // with split 2 (bf16): y's bf16 copy too
+                  void* yb = nullptr);                         // with split 2 (bf16): y's bf16 copy too;
+                                                               // split 2 with norm == nullptr: no norm
 size_t gdn_bwd_fused_ws(int C, long long P);
 int gdn_bwd_fused(const float* x, const float* norm, const float* dy, const float* gamma, int inverse, float* dx,
                   float* dgamma, float* dbeta, int C, long long P, void* ws, hipStream_t s, int split = 0,
                   float* dxsum = nullptr,   // split: 1 split dgamma, 2 bf16 operands in both GEMMs (C = 192);
-                  void* dxb = nullptr);     // dxsum: column sums of dx over all pixels (C), when non-null;
+                  void* dxb = nullptr,      // dxsum: column sums of dx over all pixels (C), when non-null;
                                             // dxb (split 2): dx's bf16 copy too
+                  const float* beta = nullptr);  // split 2 with norm == nullptr: norm recomputed from
+                                                 // x, gamma and beta (C = 192)
 
 // image-edge convolutions (edge.hip): few-channel NCHW image <-> wide NHWC maps
 bool edge_conv_ok(int C, int k, int stride, long long sw, long long ys_c, int Cout, long long ys_w, long long ys_h,

@@ -336,6 +336,51 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_xb(const Tensor& 
            "gdn_bwd_sum_xb");
   return {dx, dg, dbeta, dxsum, dxb};
 }
+// norm recomputed (C3, round 6; include/imgcomp.h ic_gdn_fwd_rn / ic_gdn_bwd_sum_rn): the forward leaves norm
+// out, the backward forms it again from x, gamma and beta.  xb: also the bf16 copy of y / dx (else an empty
+// bf16 tensor is returned in its place).
+std::tuple<Tensor, Tensor> gdn_fwd_rn(const Tensor& x, const Tensor& gamma, const Tensor& beta, bool inverse,
+                                      int64_t math, bool xb) {
+  check_operand(x, "x");
+  check_operand(gamma, "gamma");
+  check_operand(beta, "beta");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(gamma.numel() == x.size(1) * x.size(1) && beta.numel() == x.size(1), "gdn: parameters do not match ",
+              x.sizes());
+  Tensor y = at::empty_like(x);
+  Tensor yb = xb ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
+  const ic_act ax = act_of(x), ay = act_of(y);
+  const size_t nb = ic_gdn_fwd_ws_ex(&ax, (int)math);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_gdn_fwd_rn(&ax, gamma.data_ptr<float>(), beta.data_ptr<float>(), inverse ? 1 : 0, &ay,
+                         xb ? yb.data_ptr() : nullptr, (int)math, ws.data_ptr(), nb, stream_of(x)),
+           "gdn_fwd_rn");
+  return {y, yb};
+}
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_rn(const Tensor& x, const Tensor& beta, const Tensor& dy,
+                                                                  const Tensor& gamma, bool inverse, int64_t math,
+                                                                  bool xb) {
+  check_operand(x, "x");
+  check_operand(dy, "dy");
+  check_operand(beta, "beta");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "gdn_bwd_sum_rn: dy must have x's shape and strides");
+  TORCH_CHECK(beta.numel() == x.size(1), "gdn_bwd_sum_rn: beta does not match ", x.sizes());
+  Tensor dx = at::empty_like(x);
+  Tensor dg = at::empty_like(gamma, at::MemoryFormat::Contiguous);
+  Tensor dbeta = at::empty({x.size(1)}, gamma.options());
+  Tensor dxsum = at::empty({x.size(1)}, gamma.options());
+  Tensor dxb = xb ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
+  const ic_act ax = act_of(x), adx = act_of(dx);
+  const size_t nb = ic_gdn_bwd_ws(&ax);
+  Tensor ws = workspace(x, nb);
+  check_rc(ic_gdn_bwd_sum_rn(&ax, beta.data_ptr<float>(), dy.data_ptr<float>(), gamma.data_ptr<float>(),
+                             inverse ? 1 : 0, &adx, dg.data_ptr<float>(), dbeta.data_ptr<float>(),
+                             dxsum.data_ptr<float>(), xb ? dxb.data_ptr() : nullptr, (int)math, ws.data_ptr(), nb,
+                             stream_of(x)),
+           "gdn_bwd_sum_rn");
+  return {dx, dg, dbeta, dxsum, dxb};
+}
 Tensor conv2d_fwd_xb(const Tensor& x, const Tensor& xb, const Tensor& w, const c10::optional<Tensor>& b, int64_t stride,
                      int64_t pad, int64_t act, int64_t math) {
   check_operand(x, "x");
@@ -951,6 +996,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_xb_meta(const Ten
   return {at::empty_like(x), at::empty_like(gamma, at::MemoryFormat::Contiguous), at::empty({x.size(1)}, gamma.options()),
           at::empty({x.size(1)}, gamma.options()), at::empty_like(x, x.options().dtype(at::kBFloat16))};
 }
+std::tuple<Tensor, Tensor> gdn_fwd_rn_meta(const Tensor& x, const Tensor&, const Tensor&, bool, int64_t, bool xb) {
+  return {at::empty_like(x), xb ? at::empty_like(x, x.options().dtype(at::kBFloat16))
+                                : at::empty({0}, x.options().dtype(at::kBFloat16))};
+}
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> gdn_bwd_sum_rn_meta(const Tensor& x, const Tensor&, const Tensor&,
+                                                                       const Tensor& gamma, bool, int64_t, bool xb) {
+  return {at::empty_like(x), at::empty_like(gamma, at::MemoryFormat::Contiguous), at::empty({x.size(1)}, gamma.options()),
+          at::empty({x.size(1)}, gamma.options()),
+          xb ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16))};
+}
 Tensor conv2d_fwd_xb_meta(const Tensor& x, const Tensor&, const Tensor& w, const c10::optional<Tensor>& b,
                           int64_t stride, int64_t pad, int64_t act, int64_t math) {
   return conv2d_fwd_meta(x, w, b, stride, pad, act, math);
@@ -1080,6 +1135,9 @@ TORCH_LIBRARY(imgcomp, m) {
   m.def("gdn_fwd_xb(Tensor x, Tensor gamma, Tensor beta, bool inverse, int math) -> (Tensor, Tensor, Tensor)");
   m.def("gdn_bwd_sum_xb(Tensor x, Tensor norm, Tensor dy, Tensor gamma, bool inverse, int math) -> "
         "(Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("gdn_fwd_rn(Tensor x, Tensor gamma, Tensor beta, bool inverse, int math, bool xb) -> (Tensor, Tensor)");
+  m.def("gdn_bwd_sum_rn(Tensor x, Tensor beta, Tensor dy, Tensor gamma, bool inverse, int math, bool xb) -> "
+        "(Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("conv2d_fwd_xb(Tensor x, Tensor xb, Tensor weight, Tensor? bias, int stride, int padding, int act, "
         "int math) -> Tensor");
   m.def("conv_transpose2d_dgrad_xb(Tensor dy, Tensor dyb, Tensor weight, Tensor x, int stride, int padding, "
@@ -1143,6 +1201,8 @@ TORCH_LIBRARY_IMPL(imgcomp, CUDA, m) {  // the CUDA dispatch key is PyTorch-ROCm
   m.impl("gdn_bwd_sum", gdn_bwd_sum);
   m.impl("gdn_fwd_xb", gdn_fwd_xb);
   m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb);
+  m.impl("gdn_fwd_rn", gdn_fwd_rn);
+  m.impl("gdn_bwd_sum_rn", gdn_bwd_sum_rn);
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb);
   m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb);
@@ -1193,6 +1253,8 @@ TORCH_LIBRARY_IMPL(imgcomp, Meta, m) {
   m.impl("gdn_bwd_sum", gdn_bwd_sum_meta);
   m.impl("gdn_fwd_xb", gdn_fwd_xb_meta);
   m.impl("gdn_bwd_sum_xb", gdn_bwd_sum_xb_meta);
+  m.impl("gdn_fwd_rn", gdn_fwd_rn_meta);
+  m.impl("gdn_bwd_sum_rn", gdn_bwd_sum_rn_meta);
   m.impl("conv2d_fwd_xb", conv2d_fwd_xb_meta);
   m.impl("conv_transpose2d_dgrad_xb", conv_transpose2d_dgrad_xb_meta);
   m.impl("conv2d_dgrad_xb", conv2d_dgrad_xb_meta);

@@ -9,6 +9,7 @@ Layout convention: activations with >= 32 channels live in NHWC
 (torch.channels_last) so every GEMM operand row is channel-contiguous; the
 3-channel image tensors stay NCHW and take the generic gather path.
 """
+import os
 import threading
 import weakref
 
@@ -469,6 +470,16 @@ def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0
 
 
 # ============================================================== GDN
+_NORM_RECOMPUTE = os.environ.get("IMGCOMP_GDN_NORM_RECOMPUTE", "1") != "0"  # A/B knob (diagnostic)
+
+
+def _norm_recompute(x, math, math_fwd):
+    """Whether GDN leaves norm out of its forward and recomputes it in the backward: bf16 operands in
+    both directions at C = 192 (the fused bf16 kernels, config C3)."""
+    return bool(_NORM_RECOMPUTE and (int(math) & MATH["bf16"]) and (int(math_fwd) & MATH["bf16"]) and x.dim() == 4
+                and x.shape[1] == 192)
+
+
 class GDNFn(Function):
     """modelling/layers/gdn.py:84-86 given re-parameterised gamma (C,C,1,1), beta (C,)."""
 
@@ -481,11 +492,19 @@ class GDNFn(Function):
         # xb & 1: y's bf16 copy for the next conv's forward; xb & 2: dx's for the previous
         # transposed conv's input gradient (bf16 operands only; see _put_bf16)
         # (not under the eval weight cache: its convs (_cached_conv) never take the copy)
-        if (xb & 1) and (int(math_fwd) & MATH["bf16"]) and not _wcache_on(x):
+        copy = bool((xb & 1) and (int(math_fwd) & MATH["bf16"]) and not _wcache_on(x))
+        # bf16 operands at C = 192 (config C3): norm is not stored; the backward forms it again from
+        # x, gamma and beta, bitwise as the forward did (include/imgcomp.h ic_gdn_fwd_rn, round 6)
+        ctx.rn = _norm_recompute(x, math, math_fwd)
+        if ctx.rn:
+            y, yb = _lib.ops().gdn_fwd_rn(x, g, b, bool(inverse), int(math_fwd), copy)
+            norm = b  # saved in norm's place: the backward's beta
+        elif copy:
             y, norm, yb = _lib.ops().gdn_fwd_xb(x, g, b, bool(inverse), int(math_fwd))
-            _put_bf16(y, yb)
         else:
             y, norm = _lib.ops().gdn_fwd(x, g, b, bool(inverse), int(math_fwd))
+        if copy:
+            _put_bf16(y, yb)
         _log_plan("gdn_fwd", x, None, math=math_fwd)
         ctx.inverse = bool(inverse)
         ctx.math = int(math)
@@ -499,7 +518,12 @@ class GDNFn(Function):
         gy = _match(gy, x)
         # dx's column sums come with it (the fused backward forms them from its dx tiles): the
         # bias gradient of the conv that produced x, taken by that conv's backward (_take_colsum)
-        if (ctx.xb & 2) and (ctx.math & MATH["bf16"]):
+        copy = bool((ctx.xb & 2) and (ctx.math & MATH["bf16"]))
+        if ctx.rn:  # `norm` holds beta here
+            dx, dg, dbeta, dxsum, dxb = _lib.ops().gdn_bwd_sum_rn(x, norm, gy, g, ctx.inverse, ctx.math, copy)
+            if copy:
+                _put_bf16(dx, dxb)
+        elif copy:
             dx, dg, dbeta, dxsum, dxb = _lib.ops().gdn_bwd_sum_xb(x, norm, gy, g, ctx.inverse, ctx.math)
             _put_bf16(dx, dxb)
         else:

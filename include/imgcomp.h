@@ -172,6 +172,18 @@ int ic_gdn_fwd_xb(const ic_act* x, const float* gamma, const float* beta, int in
 int ic_gdn_bwd_sum_xb(const ic_act* x, const float* norm, const float* dy, const float* gamma, int inverse,
                       const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, void* dxb, int math, void* ws,
                       size_t ws_bytes, void* stream);
+/* ---- norm recomputed (config C3, round 6): the GDN forward with bf16 operands (IC_MATH_BF16 | IC_MATH_SPLIT,
+ *      C = 192, NHWC-dense) can leave norm = beta + Gamma x^2 out, and the backward forms it again per tile
+ *      from x, Gamma and beta -- the forward's operands, products and order, so bitwise the same norm.  Both
+ *      kernels are HBM-bound there; together they move 24 instead of 32 bytes per element.  yb / dxb: the
+ *      optional bf16 copies of ic_gdn_fwd_xb / ic_gdn_bwd_sum_xb (NULL: none).  Any other math mode, C or
+ *      layout is IC_ERR_ARG.  Workspaces: ic_gdn_fwd_ws_ex / ic_gdn_bwd_ws.  Replace (reference
+ *      modelling/layers/gdn.py:79-88) ic_gdn_fwd_xb / ic_gdn_bwd_sum_xb in C3's training step. */
+int ic_gdn_fwd_rn(const ic_act* x, const float* gamma, const float* beta, int inverse, const ic_act* y, void* yb,
+                  int math, void* ws, size_t ws_bytes, void* stream);
+int ic_gdn_bwd_sum_rn(const ic_act* x, const float* beta, const float* dy, const float* gamma, int inverse,
+                      const ic_act* dx, float* dgamma, float* dbeta, float* dxsum, void* dxb, int math, void* ws,
+                      size_t ws_bytes, void* stream);
 /* xb / dyb: the input's bf16 copy (NULL is an error; the workspace from *_ws_ex with math | IC_MATH_XB) */
 int ic_conv2d_fwd_xb(const ic_act* x, const void* xb, const float* w, const float* b, int k, int stride, int pad,
                      const ic_act* y, int act, int math, void* ws, size_t ws_bytes, void* stream);

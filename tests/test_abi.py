@@ -322,6 +322,9 @@ def _meta_cases():
         "gdn_fwd_xb": (lambda o: o.gdn_fwd_xb(x, _meta(192, 192), _meta(192), False, 3), [s, s, s]),
         "gdn_bwd_sum_xb": (lambda o: o.gdn_bwd_sum_xb(x, x, x, _meta(192, 192), False, 3),
                            [s, (192, 192), (192,), (192,), s]),
+        "gdn_fwd_rn": (lambda o: o.gdn_fwd_rn(x, _meta(192, 192), _meta(192), False, 3, True), [s, s]),
+        "gdn_bwd_sum_rn": (lambda o: o.gdn_bwd_sum_rn(x, _meta(192), x, _meta(192, 192), False, 3, True),
+                           [s, (192, 192), (192,), (192,), s]),
         "conv2d_fwd_xb": (lambda o: o.conv2d_fwd_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16), _meta(192, 192, 5, 5),
                                                     None, 2, 2, 0, 3), [(2, 192, 8, 8)]),
         "conv2d_wgrad_xb": (lambda o: o.conv2d_wgrad_xb(x, _meta(*s, cl=True, dtype=torch.bfloat16),

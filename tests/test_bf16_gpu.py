@@ -252,6 +252,38 @@ def test_gdn_fwd_bf16(n, h, w):
     assert e2 < e / 4  # the kernel computes what the config says, not plain fp32
 
 
+@pytest.mark.parametrize("n,h,w,inverse", [(2, 16, 16, False), (3, 7, 5, False), (4, 33, 31, True), (32, 16, 16, False)])
+def test_gdn_norm_recompute_bitwise(n, h, w, inverse):
+    """C3's GDN pair without a stored norm (round 6, include/imgcomp.h ic_gdn_fwd_rn / ic_gdn_bwd_sum_rn):
+    the forward leaves norm out and the backward forms it again per tile from x, Gamma and beta with the
+    forward's bf16 operands and MFMA order -- so y, its bf16 copy, dx, dx's copy, dGamma, dbeta and the dx
+    column sums are bitwise those of the pair that stores norm (ragged pixel counts, IGDN, the 4-tile
+    split across the two wave groups, and a C3-sized 16^2 layer).  The model path takes it whenever
+    both directions run on bf16 operands at C = 192 (functional._norm_recompute)."""
+    from image_compression_amd import _lib
+    ops = _lib.ops()
+    g = torch.Generator().manual_seed(31)
+    x = (torch.randn(n, 192, h, w, generator=g)).to(DEV).contiguous(memory_format=torch.channels_last)
+    dy = (torch.randn(n, 192, h, w, generator=g)).to(DEV).contiguous(memory_format=torch.channels_last)
+    gamma = (torch.eye(192) * 0.1 + torch.rand(192, 192, generator=g) * 0.01).reshape(192, 192, 1, 1).to(DEV)
+    beta = (1.0 + torch.rand(192, generator=g) * 0.1).to(DEV)
+    for xb in (True, False):
+        y0, norm, yb0 = ops.gdn_fwd_xb(x, gamma, beta, inverse, 3)
+        y1, yb1 = ops.gdn_fwd_rn(x, gamma, beta, inverse, 3, xb)
+        assert torch.equal(y0, y1)
+        if xb:
+            assert torch.equal(yb0, yb1)
+        r0 = ops.gdn_bwd_sum_xb(x, norm, dy, gamma, inverse, 3)
+        r1 = ops.gdn_bwd_sum_rn(x, beta, dy, gamma, inverse, 3, xb)
+        for i, nm in enumerate(("dx", "dgamma", "dbeta", "dxsum", "dxb")):
+            if nm == "dxb" and not xb:
+                continue
+            assert torch.equal(r0[i], r1[i]), (nm, xb, (r0[i].float() - r1[i].float()).abs().max().item())
+    # any other arithmetic refuses the norm-free form
+    with pytest.raises(RuntimeError):
+        ops.gdn_fwd_rn(x, gamma, beta, inverse, 2, False)
+
+
 def test_c3_bf16_copies_bitwise():
     """Config C3's bf16 activation copies (round 5): every GDN / IGDN of g_a and g_s whose output feeds
     a 192-output conv or transposed conv writes that output's bf16 copy for the conv's forward, and
