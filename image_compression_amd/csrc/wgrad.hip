@@ -739,7 +739,8 @@ __global__ void __launch_bounds__(256, TWO ? 2 : 1) wg_x3_kernel(const WgDesc d)
 #endif
 #ifndef WG_X3P_ABL
 #define WG_X3P_ABL 0  // diagnostic ablations of wg_x3p_kernel (wrong results): 1 no global loads, 2 no LDS stores, 4 no MFMAs, 8 every step loads the split's first pixels (L2-hot), 16 no split (one
-// conversion per value), 32 every step loads step 0 (loop-invariant addresses)
+// conversion per value), 32 every step loads step 0 (loop-invariant addresses), 64 G stored unsplit (one
+// conversion per G value, X split as usual: round 6, what G pre-split into three planes could save)
 #endif
 #ifndef WG_X3_DUAL16
 #define WG_X3_DUAL16 1  // the two-wave kernel also on maps 16 wide (two row segments per step)
@@ -1083,8 +1084,8 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
         okm |= ok ? 2u << q : 0u;
       }
     };
-    auto put = [&](__bf16* dst, int plane, floatx4v v) {
-      if constexpr (NP == 1 || (WG_X3P_ABL & 16)) {
+    auto put = [&](__bf16* dst, int plane, floatx4v v, bool gop = false) {
+      if (NP == 1 || (WG_X3P_ABL & 16) || ((WG_X3P_ABL & 64) && gop)) {  // ABL 64: G stored unsplit (diagnostic)
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         *(b4*)dst = __builtin_bit_cast(b4, u32x2{ic_cvt_pk_bf16(v[0], v[1]), ic_cvt_pk_bf16(v[2], v[3])});
       } else {
@@ -1111,7 +1112,7 @@ __device__ __forceinline__ void wg_x3p_body(const WgDesc& d, __bf16* lds, int sp
       } else {
 #pragma unroll
       for (int q = 0; q < QG; ++q) {
-        put(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q])), GPLANE, (okm & 1u) ? rg[q] : zero4);
+        put(base + grow[q] * PITCH + (gcol[q] ^ swz(grow[q])), GPLANE, (okm & 1u) ? rg[q] : zero4, true);
         __builtin_amdgcn_sched_barrier(0);  // one slot at a time: the split temporaries of ten slots spilled
       }
 #pragma unroll
