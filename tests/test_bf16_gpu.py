@@ -44,6 +44,46 @@ def test_conv_bf16_fwd_dgrad(cin, cout, hw, k, s):
     assert rel_err(wd.grad.cpu(), wr.grad) < 1e-5   # weight gradient stays fp32 on maps < 16 wide
 
 
+@pytest.mark.parametrize("case", ["conv_ragged_ksplit", "conv_four_phase_dgrad", "tconv_four_phase_fwd",
+                                  "tconv_ksplit_dgrad"])
+def test_b16d_vs_bf16_emulation(case):
+    """ig_kernel_b16d (the C3 bf16 DMA tiles) in isolation at 1e-5 against fp64 of the same bf16-rounded
+    operands (oracle.ref_cpu._ConvRounded): a one-phase conv forward with a ragged last tile and K split
+    (41 tiles of 256 rows), a stride-2 conv's four-phase input gradient (272 tiles), the four-phase
+    transposed-conv forward, and the transposed conv's one-phase input gradient with K split; each
+    asserts the plan it ran (advisor round 5: these had been held only at the 1e-2 bar)."""
+    from image_compression_amd import _lib, functional as IF
+    from oracle import ref_cpu
+    torch.set_num_threads(16)
+    tr = case.startswith("tconv")
+    n, hw = {"conv_ragged_ksplit": (5, (90, 94)), "conv_four_phase_dgrad": (4, (128, 136)),
+             "tconv_four_phase_fwd": (4, (64, 68)), "tconv_ksplit_dgrad": (4, (64, 68))}[case]
+    x = _r(n, 192, *hw, seed=41)
+    w = _r(192, 192, 5, 5, seed=42, scale=0.03)
+    b = _r(192, seed=43, scale=0.1)
+    xe = x.double().requires_grad_(True)
+    ye = ref_cpu._ConvRounded.apply(xe, w.double(), b.double(), 2, 2, 1 if tr else 0, tr, True, True, False)
+    gy = _r(*ye.shape, seed=44)
+    ye.backward(gy.double())
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(DEV)
+    if tr:
+        y = IF.conv_transpose2d(xd, wd, b.to(DEV), 2, 2, 1, math=1)
+    else:
+        y = IF.conv2d(xd, wd, b.to(DEV), 2, 2, math=1)
+    gyd = gy.to(DEV).contiguous(memory_format=torch.channels_last)
+    y.backward(gyd)
+    op = {"conv_ragged_ksplit": ("conv2d_fwd", xd, y), "conv_four_phase_dgrad": ("conv2d_dgrad", gyd, xd),
+          "tconv_four_phase_fwd": ("conv_transpose2d_fwd", xd, y), "tconv_ksplit_dgrad": ("conv_transpose2d_dgrad", gyd, xd)}[case]
+    plan = _lib.plan(op[0], op[1].detach(), op[2].detach(), 5, 2, 2, 1)
+    assert plan["kernel"] == "ig_bf16_dma", plan
+    if case in ("conv_ragged_ksplit", "tconv_ksplit_dgrad"):
+        assert plan["ksplit"] > 1, plan
+    ey, edx = rel_err(y.detach().cpu(), ye.detach()), rel_err(xd.grad.cpu(), xe.grad)
+    print(f"{case}: y {ey:.2e}, dx {edx:.2e} vs fp64 of the bf16 operands; plan {plan}")
+    assert ey < 1e-5 and edx < 1e-5, (ey, edx)
+
+
 @pytest.mark.parametrize("transposed", [False, True])
 def test_wgrad_bf16(transposed):
     """Weight gradients with bf16 operands (the two-wave kernel with one product per tile and
