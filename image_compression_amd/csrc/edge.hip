@@ -290,7 +290,10 @@ constexpr int EC3_KP = 32 * EC3_S;       // k columns of the B planes (96)
 constexpr int EC3_PL = SEG * EC3_KP;     // bf16 per plane
 // NP = 1 (IC_MATH_BF16, config C3): bf16 operands (weights and patch values rounded to nearest
 // even), one plane, one product per tile and k-step, fp32 accumulation.
-template <int COUT, int NP = 3>
+// SC: the k-step count S = ceil(T*C / 32) when known at compile time (3: the 3-channel 5x5 edges of
+// every config), 0 = read from the geometry.  A compile-time S leaves no branch between the k-steps'
+// MFMA groups, so the next k-step's fragment reads issue under the current one's MFMAs.
+template <int COUT, int NP = 3, int SC = 0>
 __global__ void __launch_bounds__(512, 1)
     edge_conv_x3_kernel(const EdgeGeom g, const float* __restrict__ wp, int Kp, const float* __restrict__ bias,
                         int relu, float* __restrict__ y, long long ys_n, long long ys_h, long long ys_w) {
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(512, 1)
   const int li = lane & 15, lq = lane >> 4;
   const int nbase = (w & 3) * (COUT / 4);
   const int mt0 = 2 * (w >> 2);
-  const int S = (g.TC + 31) / 32;
+  const int S = SC ? SC : (g.TC + 31) / 32;
   const int PSZ = g.C * g.k * g.PW;
   const int zero_off = PSZ;
   const int bufsz = PMAX + 2 * SEG * 2;
@@ -1055,11 +1058,18 @@ int edge_conv_run(const float* x, long long sn, long long sc, long long sh, long
   if (edge_conv_split(split, g.TC, Cout)) {
     const int grid1 = edge_grid(g.units, 1);
     if (grid1 < 1) return IC_OK;
+    const bool s3 = (g.TC + 31) / 32 == 3;
 #define EDGE_CONV_X3(CO_)                                                                                      \
   do {                                                                                                         \
-    if (split == 2)                                                                                            \
+    if (split == 2 && s3)                                                                                      \
+      hipLaunchKernelGGL((edge_conv_x3_kernel<CO_, 1, 3>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, \
+                         y, ys_n, ys_h, ys_w);                                                                 \
+    else if (split == 2)                                                                                       \
       hipLaunchKernelGGL((edge_conv_x3_kernel<CO_, 1>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y, \
                          ys_n, ys_h, ys_w);                                                                    \
+    else if (s3)                                                                                               \
+      hipLaunchKernelGGL((edge_conv_x3_kernel<CO_, 3, 3>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, \
+                         y, ys_n, ys_h, ys_w);                                                                 \
     else                                                                                                       \
       hipLaunchKernelGGL((edge_conv_x3_kernel<CO_>), dim3(grid1), dim3(512), 0, s, g, wp, Kp, bias, relu, y,    \
                          ys_n, ys_h, ys_w);                                                                    \
