@@ -34,16 +34,17 @@ class ICFactGrads(ctypes.Structure):
     _fields_ = [(f, c_void) for f in _FACT_FIELDS]
 
 
-FACT_MAXL, FACT_MAXW = 6, 8  # IC_FACT_MAXL / IC_FACT_MAXW
+FACT_MAXL, FACT_MAXW = 6, 8  # IC_FACT_MAXL / IC_FACT_MAXW: the register kernels
+FACT_NET_MAXL, FACT_WIDE_MAXW = 32, 256  # IC_FACT_NET_MAXL / IC_FACT_WIDE_MAXW: the wide kernels (any geometry)
 
 
 class ICFactNet(ctypes.Structure):
-    _fields_ = [("nlayers", c_int), ("dims", c_int * (FACT_MAXL + 1)), ("w", c_void * FACT_MAXL),
-                ("b", c_void * FACT_MAXL), ("f", c_void * FACT_MAXL)]
+    _fields_ = [("nlayers", c_int), ("dims", c_int * (FACT_NET_MAXL + 1)), ("w", c_void * FACT_NET_MAXL),
+                ("b", c_void * FACT_NET_MAXL), ("f", c_void * FACT_NET_MAXL)]
 
 
 class ICFactNetGrads(ctypes.Structure):
-    _fields_ = [("w", c_void * FACT_MAXL), ("b", c_void * FACT_MAXL), ("f", c_void * FACT_MAXL)]
+    _fields_ = [("w", c_void * FACT_NET_MAXL), ("b", c_void * FACT_NET_MAXL), ("f", c_void * FACT_NET_MAXL)]
 
 
 class ICAdamWTensor(ctypes.Structure):
@@ -165,6 +166,11 @@ SIGNATURES = {
                                       c_void, c_void]),
     "ic_factorized_bwd_net": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_void, c_void, c_void,
                                       P(ICFactNetGrads), c_void]),
+    "ic_factorized_net_ws": (c_size, [c_ll, c_int, P(ICFactNet), c_int]),
+    "ic_factorized_fwd_net_ex": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_int, c_void, c_ull, c_ull,
+                                         c_void, c_void, c_void, c_size, c_void]),
+    "ic_factorized_bwd_net_ex": (c_int, [c_void, c_ll, c_int, P(ICFactNet), c_float, c_void, c_void, c_void,
+                                         P(ICFactNetGrads), c_void, c_size, c_void]),
     "ic_msssim_state_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "ic_msssim_ws": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "ic_msssim_fwd": (c_int, [c_void, c_void, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int,

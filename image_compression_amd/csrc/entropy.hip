@@ -555,12 +555,21 @@ __global__ void quant_k(const float* y, long long n, int mode, const float* u, u
   }
 }
 
-bool fact_net_ok(const ic_fact_net* N) {
-  if (!N || N->nlayers < 1 || N->nlayers > FML || N->dims[0] != 1 || N->dims[N->nlayers] != 1) return false;
+// a well-formed net the wide kernels take (up to IC_FACT_NET_MAXL layers of width <= IC_FACT_WIDE_MAXW)
+bool fact_net_valid(const ic_fact_net* N) {
+  if (!N || N->nlayers < 1 || N->nlayers > IC_FACT_NET_MAXL || N->dims[0] != 1 || N->dims[N->nlayers] != 1)
+    return false;
   for (int l = 0; l < N->nlayers; ++l) {
-    if (N->dims[l + 1] < 1 || N->dims[l + 1] > FMW || !N->w[l] || !N->b[l]) return false;
+    if (N->dims[l + 1] < 1 || N->dims[l + 1] > IC_FACT_WIDE_MAXW || !N->w[l] || !N->b[l]) return false;
     if (l < N->nlayers - 1 && !N->f[l]) return false;
   }
+  return true;
+}
+// ... within the register kernels' limits
+bool fact_net_ok(const ic_fact_net* N) {
+  if (!fact_net_valid(N) || N->nlayers > FML) return false;
+  for (int l = 0; l < N->nlayers; ++l)
+    if (N->dims[l + 1] > FMW) return false;
   return true;
 }
 
@@ -572,6 +581,240 @@ size_t fact_net_lds(const ic_fact_net* N, bool bwd) {
     row += 2 * dout + din;
   }
   return ((size_t)prm + (bwd ? (size_t)FNT * row + FNT : 0)) * sizeof(float);
+}
+
+// ---------------------------------------------------------------- CDF MLP of any geometry (wide)
+// Nets past the register kernels' limits (more than IC_FACT_MAXL layers or a hidden width above
+// IC_FACT_MAXW; entropy_model.py:88-99 builds any DIMS), up to IC_FACT_NET_MAXL layers of width <=
+// IC_FACT_WIDE_MAXW: the register kernels' arithmetic in the same order (a layer's products summed
+// over its inputs in index order, the same gate and sigmoid formulas), with each thread's activations
+// in a scratch of the workspace instead of registers and the channel's transformed parameters
+// (softplus W, b, tanh f) formed once per call into the workspace.  One wave per channel.  Backward as
+// fact_bwd_net_k: per round of FW / 2 elements, lane t backpropagates evaluation t & 1 of element t >> 1
+// and writes its per-layer terms to row t (in the workspace); after the barrier each lane sums the
+// terms of the parameters it owns over the rows in row order -- deterministic, no atomics.
+constexpr int FW = 64;
+struct WideLayout {
+  int ow[IC_FACT_NET_MAXL], ob[IC_FACT_NET_MAXL], of[IC_FACT_NET_MAXL];  // parameter offsets per layer
+  int rd[IC_FACT_NET_MAXL], rg[IC_FACT_NET_MAXL], rh[IC_FACT_NET_MAXL];  // row offsets: delta, gate term, input
+  int aa[IC_FACT_NET_MAXL], ah[IC_FACT_NET_MAXL];                        // activation record: pre-gate, input
+  int np, nrow, nact, wmax;
+};
+
+WideLayout wide_layout(const ic_fact_net& N) {
+  WideLayout F{};
+  int o = 0, r = 0, a = 0, wm = 1;
+  for (int l = 0; l < N.nlayers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    F.ow[l] = o; o += dout * din;
+    F.ob[l] = o; o += dout;
+    F.of[l] = o; o += l < N.nlayers - 1 ? dout : 0;
+    F.rd[l] = r; r += dout;
+    F.rg[l] = r; r += dout;
+    F.rh[l] = r; r += din;
+    F.aa[l] = a; a += dout;
+    F.ah[l] = a; a += din;
+    wm = max(wm, dout);
+  }
+  F.np = o; F.nrow = r; F.nact = a; F.wmax = wm;
+  return F;
+}
+
+// workspace (floats): transformed parameters [C][np]; per lane of each channel's wave: the evaluation
+// scratch (2 wmax), and in the backward the activation record (nact), its row (nrow), plus [C][np]
+// parameter sums
+struct WideWs {
+  size_t tp, scr, act, rows, acc, total;
+};
+WideWs wide_ws(int C, const WideLayout& F, bool bwd) {
+  WideWs w{};
+  size_t o = 0;
+  auto take = [&](size_t floats) { const size_t at = o; o += ic_align(floats * 4, 256); return at; };
+  w.tp = take((size_t)C * F.np);
+  w.scr = take((size_t)C * FW * 2 * F.wmax);
+  if (bwd) {
+    w.act = take((size_t)C * FW * F.nact);
+    w.rows = take((size_t)C * FW * F.nrow);
+    w.acc = take((size_t)C * F.np);
+  }
+  w.total = o;
+  return w;
+}
+
+__global__ void __launch_bounds__(FW) fact_wide_prep_k(const ic_fact_net N, const WideLayout F, float* __restrict__ tp) {
+  const int c = blockIdx.x;
+  float* t = tp + (size_t)c * F.np;
+  for (int l = 0; l < N.nlayers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    for (int j = threadIdx.x; j < dout * din; j += FW) t[F.ow[l] + j] = softplusf(N.w[l][(size_t)c * dout * din + j]);
+    for (int j = threadIdx.x; j < dout; j += FW) {
+      t[F.ob[l] + j] = N.b[l][(size_t)c * dout + j];
+      if (l < N.nlayers - 1) t[F.of[l] + j] = tanhf(N.f[l][(size_t)c * dout + j]);
+    }
+  }
+}
+
+// logits of one evaluation at v (as fact_eval); act != nullptr records each layer's input and pre-gate values
+__device__ float wide_eval(const ic_fact_net& N, const WideLayout& F, const float* __restrict__ tp, float v,
+                           float* h, float* hn, float* act) {
+  h[0] = v;
+  for (int l = 0; l < N.nlayers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    const bool gate = l < N.nlayers - 1;
+    if (act)
+      for (int i = 0; i < din; ++i) act[F.ah[l] + i] = h[i];
+    for (int o = 0; o < dout; ++o) {
+      float s = tp[F.ob[l] + o];
+      const float* w = tp + F.ow[l] + o * din;
+      for (int i = 0; i < din; ++i) s += w[i] * h[i];
+      if (act) act[F.aa[l] + o] = s;
+      hn[o] = gate ? s + tanhf(s) * tp[F.of[l] + o] : s;
+    }
+    float* t = h; h = hn; hn = t;
+  }
+  return h[0];
+}
+
+__global__ void __launch_bounds__(FW) fact_fwd_wide_k(const float* z, long long n, int C, const ic_fact_net N,
+                                                      const WideLayout F, float half, int mode, const float* u,
+                                                      unsigned long long seed, unsigned long long off, float* qo,
+                                                      float* po, const float* __restrict__ tp_all, float* scr_all) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const float* tp = tp_all + (size_t)c * F.np;
+  float* h = scr_all + ((size_t)c * FW + t) * 2 * F.wmax;
+  const long long ne = n / C;
+  for (long long e = t; e < ne; e += FW) {
+    const long long i = e * C + c;
+    float qv;
+    if (mode == 1) {
+      qv = rintf(z[i]);
+    } else {
+      float uu;
+      if (mode == 0) uu = u[i];
+      else if (mode == 3) {
+        const unsigned long long* st = (const unsigned long long*)u;
+        uu = philox_uniform(st[0], st[1] + off + (unsigned long long)i);
+      } else {
+        uu = philox_uniform(seed, off + (unsigned long long)i);
+      }
+      qv = z[i] + (uu - half);
+    }
+    qo[i] = qv;
+    const float lo = wide_eval(N, F, tp, qv - half, h, h + F.wmax, nullptr);
+    const float up = wide_eval(N, F, tp, qv + half, h, h + F.wmax, nullptr);
+    const float s = -signf_(lo + up);
+    po[i] = s * (sigmoidf_(up * s) - sigmoidf_(lo * s));
+  }
+}
+
+// the rows term of parameter j: row[oa] * (ob < 0 ? 1 : row[ob]) (fact_bwd_net_k's ownership map)
+__device__ void wide_param_rows(const ic_fact_net& N, const WideLayout& F, int j, int& oa, int& ob) {
+  oa = -1; ob = -1;
+  for (int l = 0; l < N.nlayers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    const int nl = dout * din + dout + (l < N.nlayers - 1 ? dout : 0);
+    if (j >= nl) { j -= nl; continue; }
+    if (j < dout * din) { oa = F.rd[l] + j / din; ob = F.rh[l] + j % din; }
+    else if (j < dout * din + dout) { oa = F.rd[l] + (j - dout * din); }
+    else { oa = F.rg[l] + (j - dout * din - dout); }
+    return;
+  }
+}
+
+__global__ void __launch_bounds__(FW) fact_bwd_wide_k(const float* qin, long long n, int C, const ic_fact_net N,
+                                                      const WideLayout F, float half, const float* dq, const float* dp,
+                                                      float* dz, const ic_fact_net_grads GR,
+                                                      const float* __restrict__ tp_all, float* scr_all, float* act_all,
+                                                      float* rows_all, float* acc_all) {
+  __shared__ float dvb[FW];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const float* tp = tp_all + (size_t)c * F.np;
+  float* h = scr_all + ((size_t)c * FW + t) * 2 * F.wmax;  // evaluation scratch, then dh / da
+  float* act = act_all + ((size_t)c * FW + t) * F.nact;
+  float* rows = rows_all + (size_t)c * FW * F.nrow;
+  float* row = rows + (size_t)t * F.nrow;
+  float* acc = acc_all + (size_t)c * F.np;
+  for (int j = t; j < F.np; j += FW) acc[j] = 0.f;
+  const long long ne = n / C;
+  const int which = t & 1;  // 0: lower (q - half), 1: upper (q + half)
+  for (long long e0 = 0; e0 < ne; e0 += FW / 2) {
+    const long long e = e0 + (t >> 1);
+    float dv = 0.f;
+    const bool live = e < ne;
+    const long long i = e * C + c;
+    const float gp = (live && dp) ? dp[i] : 0.f;
+    if (live && gp != 0.f) {
+      const float qv = qin[i];
+      const float lo = wide_eval(N, F, tp, qv - half, h, h + F.wmax, which ? nullptr : act);
+      const float up = wide_eval(N, F, tp, qv + half, h, h + F.wmax, which ? act : nullptr);
+      const float s = -signf_(lo + up);
+      const float su = sigmoidf_(s * up), sl = sigmoidf_(s * lo);
+      // p = s (sig(s up) - sig(s lo)), s detached
+      const float g = which ? gp * s * su * (1.f - su) * s : -gp * s * sl * (1.f - sl) * s;
+      float* dh = h;
+      float* da = h + F.wmax;
+      dh[0] = g;
+      for (int l = N.nlayers - 1; l >= 0; --l) {
+        const int din = N.dims[l], dout = N.dims[l + 1];
+        const bool gate = l < N.nlayers - 1;
+        for (int o = 0; o < dout; ++o) {
+          float d;
+          if (gate) {
+            const float th = tanhf(act[F.aa[l] + o]);
+            d = dh[o] * (1.f + (1.f - th * th) * tp[F.of[l] + o]);
+            row[F.rg[l] + o] = dh[o] * th;
+          } else {
+            d = dh[o];
+            row[F.rg[l] + o] = 0.f;
+          }
+          row[F.rd[l] + o] = d;
+          da[o] = d;
+        }
+        for (int i2 = 0; i2 < din; ++i2) {
+          row[F.rh[l] + i2] = act[F.ah[l] + i2];
+          float sacc = 0.f;
+          for (int o = 0; o < dout; ++o) sacc += tp[F.ow[l] + o * din + i2] * da[o];
+          dh[i2] = sacc;
+        }
+      }
+      dv = dh[0];
+    } else {
+      for (int r = 0; r < F.nrow; ++r) row[r] = 0.f;
+    }
+    dvb[t] = dv;
+    __syncthreads();  // the rows (workspace) and dvb: visible to the whole wave
+    if (live && which == 0 && dz) dz[i] = (dq ? dq[i] : 0.f) + (dvb[t] + dvb[t + 1]);
+    for (int j = t; j < F.np; j += FW) {
+      int oa, ob;
+      wide_param_rows(N, F, j, oa, ob);
+      float sacc = 0.f;
+      for (int r = 0; r < FW; ++r) {
+        const float* rr = rows + (size_t)r * F.nrow;
+        sacc += ob < 0 ? rr[oa] : rr[oa] * rr[ob];
+      }
+      acc[j] += sacc;
+    }
+    __syncthreads();
+  }
+  // raw sums -> parameter gradients (softplus' for W, 1 - tanh^2 for f)
+  for (int j0 = t; j0 < F.np; j0 += FW) {
+    int j = j0;
+    for (int l = 0; l < N.nlayers; ++l) {
+      const int din = N.dims[l], dout = N.dims[l + 1];
+      const int nl = dout * din + dout + (l < N.nlayers - 1 ? dout : 0);
+      if (j >= nl) { j -= nl; continue; }
+      if (j < dout * din) {
+        GR.w[l][(size_t)c * dout * din + j] = acc[j0] * dsoftplusf(N.w[l][(size_t)c * dout * din + j]);
+      } else if (j < dout * din + dout) {
+        GR.b[l][(size_t)c * dout + (j - dout * din)] = acc[j0];
+      } else {
+        const int o = j - dout * din - dout;
+        const float tf = tanhf(N.f[l][(size_t)c * dout + o]);
+        GR.f[l][(size_t)c * dout + o] = acc[j0] * (1.f - tf * tf);
+      }
+      break;
+    }
+  }
 }
 
 }  // namespace
@@ -647,28 +890,69 @@ int ic_conditional_bwd(const float* q, const float* scale, const float* mean, lo
   return ic_conditional_bwd_bin(q, scale, mean, n, kind, 1.f, dq, dp, dy, dscale, dmean, stream);
 }
 
-int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
-                          const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
-                          void* stream) {
-  if (C <= 0 || n % C != 0 || (mode == 0 && !u) || !fact_net_ok(net) || !(bin > 0.f)) return IC_ERR_ARG;
+size_t ic_factorized_net_ws(long long n, int C, const ic_fact_net* net, int bwd) {
+  (void)n;
+  if (C <= 0 || !fact_net_valid(net)) return 0;
+  if (fact_net_ok(net) && fact_net_lds(net, bwd != 0) <= 160 * 1024) return 0;  // the register kernels
+  return wide_ws(C, wide_layout(*net), bwd != 0).total;
+}
+
+int ic_factorized_fwd_net_ex(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
+                             const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                             void* ws, size_t ws_bytes, void* stream) {
+  if (C <= 0 || n % C != 0 || (mode == 0 && !u) || !fact_net_valid(net) || !(bin > 0.f)) return IC_ERR_ARG;
   if ((mode == 2 || mode == 3) && (offset & 3)) return IC_ERR_ARG;  // whole Philox blocks
-  hipLaunchKernelGGL(fact_fwd_net_k, dim3(C), dim3(FNT), fact_net_lds(net, false), (hipStream_t)stream, z, n, C,
-                     *net, 0.5f * bin, mode, u, seed, offset, q, p);
+  if (fact_net_ok(net)) {
+    hipLaunchKernelGGL(fact_fwd_net_k, dim3(C), dim3(FNT), fact_net_lds(net, false), (hipStream_t)stream, z, n, C,
+                       *net, 0.5f * bin, mode, u, seed, offset, q, p);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
+  const WideLayout F = wide_layout(*net);
+  const WideWs W = wide_ws(C, F, false);
+  if (!ws || ws_bytes < W.total) return IC_ERR_WORKSPACE;
+  char* b = (char*)ws;
+  hipLaunchKernelGGL(fact_wide_prep_k, dim3(C), dim3(FW), 0, (hipStream_t)stream, *net, F, (float*)(b + W.tp));
+  hipLaunchKernelGGL(fact_fwd_wide_k, dim3(C), dim3(FW), 0, (hipStream_t)stream, z, n, C, *net, F, 0.5f * bin, mode, u,
+                     seed, offset, q, p, (const float*)(b + W.tp), (float*)(b + W.scr));
   IC_CHECK_LAUNCH();
   return IC_OK;
 }
 
-int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
-                          const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream) {
-  if (C <= 0 || n % C != 0 || !fact_net_ok(net) || !grd || !(bin > 0.f)) return IC_ERR_ARG;
+int ic_factorized_bwd_net_ex(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
+                             const float* dp, float* dz, const ic_fact_net_grads* grd, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (C <= 0 || n % C != 0 || !fact_net_valid(net) || !grd || !(bin > 0.f)) return IC_ERR_ARG;
   for (int l = 0; l < net->nlayers; ++l)
     if (!grd->w[l] || !grd->b[l] || (l < net->nlayers - 1 && !grd->f[l])) return IC_ERR_ARG;
   const size_t lds = fact_net_lds(net, true);
-  if (lds > 160 * 1024) return IC_ERR_ARG;
-  hipLaunchKernelGGL(fact_bwd_net_k, dim3(C), dim3(FNT), lds, (hipStream_t)stream, q, n, C, *net, 0.5f * bin, dq, dp,
-                     dz, *grd);
+  if (fact_net_ok(net) && lds <= 160 * 1024) {
+    hipLaunchKernelGGL(fact_bwd_net_k, dim3(C), dim3(FNT), lds, (hipStream_t)stream, q, n, C, *net, 0.5f * bin, dq,
+                       dp, dz, *grd);
+    IC_CHECK_LAUNCH();
+    return IC_OK;
+  }
+  const WideLayout F = wide_layout(*net);
+  const WideWs W = wide_ws(C, F, true);
+  if (!ws || ws_bytes < W.total) return IC_ERR_WORKSPACE;
+  char* b = (char*)ws;
+  hipLaunchKernelGGL(fact_wide_prep_k, dim3(C), dim3(FW), 0, (hipStream_t)stream, *net, F, (float*)(b + W.tp));
+  hipLaunchKernelGGL(fact_bwd_wide_k, dim3(C), dim3(FW), 0, (hipStream_t)stream, q, n, C, *net, F, 0.5f * bin, dq, dp,
+                     dz, *grd, (const float*)(b + W.tp), (float*)(b + W.scr), (float*)(b + W.act),
+                     (float*)(b + W.rows), (float*)(b + W.acc));
   IC_CHECK_LAUNCH();
   return IC_OK;
+}
+
+int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
+                          const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                          void* stream) {
+  return ic_factorized_fwd_net_ex(z, n, C, net, bin, mode, u, seed, offset, q, p, nullptr, 0, stream);
+}
+
+int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
+                          const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream) {
+  return ic_factorized_bwd_net_ex(q, n, C, net, bin, dq, dp, dz, grd, nullptr, 0, stream);
 }
 
 }  // extern "C"

@@ -771,7 +771,8 @@ std::tuple<Tensor, std::vector<Tensor>> factorized_bwd(const Tensor& q, int64_t 
 // any CDF MLP: dims = {1, DIMS..., 1}; params [w0, b0, f0, w1, b1, f1, ..., w_last, b_last]
 ic_fact_net fact_net(at::IntArrayRef dims, at::TensorList prm) {
   const int L = (int)dims.size() - 1;
-  TORCH_CHECK(L >= 1 && L <= IC_FACT_MAXL, "factorized: CDF MLP of ", L, " layers (at most ", IC_FACT_MAXL, ")");
+  TORCH_CHECK(L >= 1 && L <= IC_FACT_NET_MAXL, "factorized: CDF MLP of ", L, " layers (at most ", IC_FACT_NET_MAXL,
+              ")");
   TORCH_CHECK((int64_t)prm.size() == 3 * L - 1, "factorized: expected ", 3 * L - 1, " CDF parameter tensors");
   ic_fact_net net{};
   net.nlayers = L;
@@ -798,9 +799,12 @@ std::tuple<Tensor, Tensor> factorized_net_fwd(const Tensor& z, int64_t C, at::In
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(z.device());
   const ic_fact_net net = fact_net(dims, prm);
   Tensor q = like(z), p = like(z);
-  check_rc(ic_factorized_fwd_net(z.data_ptr<float>(), z.numel(), (int)C, &net, (float)bin, (int)mode,
-                                 (const float*)noise_ptr(u, mode, z), (unsigned long long)seed,
-                                 (unsigned long long)offset, q.data_ptr<float>(), p.data_ptr<float>(), stream_of(z)),
+  const size_t nb = ic_factorized_net_ws(z.numel(), (int)C, &net, 0);  // 0: the register kernels
+  Tensor ws = workspace(z, nb);
+  check_rc(ic_factorized_fwd_net_ex(z.data_ptr<float>(), z.numel(), (int)C, &net, (float)bin, (int)mode,
+                                    (const float*)noise_ptr(u, mode, z), (unsigned long long)seed,
+                                    (unsigned long long)offset, q.data_ptr<float>(), p.data_ptr<float>(),
+                                    ws.data_ptr(), nb, stream_of(z)),
            "factorized_net_fwd");
   return {q, p};
 }
@@ -824,8 +828,10 @@ std::tuple<Tensor, std::vector<Tensor>> factorized_net_bwd(const Tensor& q, int6
     k += l < L - 1 ? 3 : 2;
   }
   Tensor dz = like(q);
-  check_rc(ic_factorized_bwd_net(q.data_ptr<float>(), q.numel(), (int)C, &net, (float)bin, opt_grad(dq, q, "dq"),
-                                 opt_grad(dp, q, "dp"), dz.data_ptr<float>(), &g, stream_of(q)),
+  const size_t nb = ic_factorized_net_ws(q.numel(), (int)C, &net, 1);
+  Tensor ws = workspace(q, nb);
+  check_rc(ic_factorized_bwd_net_ex(q.data_ptr<float>(), q.numel(), (int)C, &net, (float)bin, opt_grad(dq, q, "dq"),
+                                    opt_grad(dp, q, "dp"), dz.data_ptr<float>(), &g, ws.data_ptr(), nb, stream_of(q)),
            "factorized_net_bwd");
   return {dz, grads};
 }

@@ -740,14 +740,16 @@ class FactorizedFn(Function):
 
 class FactorizedNetFn(Function):
     """EntropyModel with any CDF MLP widths (cfg DIMS) and any BIN (entropy_model.py:88-99,
-    :198, :229-232, :259-269) on the generic kernels (torch.ops.imgcomp.factorized_net_*)."""
+    :198, :229-232, :259-269) on the generic kernels (torch.ops.imgcomp.factorized_net_*): the
+    register kernels up to 5 hidden layers of width <= 8, the wide kernels beyond (up to 31 hidden
+    layers of width <= 256)."""
 
     @staticmethod
     def forward(ctx, z, mode, u, seed, offset, dims, bin_, *params):
         _lib.require_device(z, None if mode == 3 else u, *params)
-        if len(dims) - 1 > _lib.FACT_MAXL or max(dims[1:-1] or [1]) > _lib.FACT_MAXW:
-            raise NotImplementedError(f"CDF MLP dims {list(dims)}: the generic kernel takes <= {_lib.FACT_MAXL} "
-                                      f"layers of width <= {_lib.FACT_MAXW}")
+        if len(dims) - 1 > _lib.FACT_NET_MAXL or max(dims[1:-1] or [1]) > _lib.FACT_WIDE_MAXW:
+            raise NotImplementedError(f"CDF MLP dims {list(dims)}: the kernels take <= {_lib.FACT_NET_MAXL} "
+                                      f"layers of width <= {_lib.FACT_WIDE_MAXW}")
         C = z.shape[1]
         zl = _to_last(z)
         prm = [t.contiguous() for t in params]

@@ -5,8 +5,10 @@ models on y (:272-378).  Noise/round + likelihood run in fused HIP kernels
 (csrc/entropy.hip): the factorized CDF MLP (1->3->3->3->1 per channel, softplus
 weights, tanh gates) is evaluated twice per element in registers, and the
 per-channel parameter gradients are deterministic block reductions.  Other
-cfg.MODEL.ENTROPY_MODEL.DIMS (up to 5 hidden layers of width <= 8) and any
-BIN run the generic kernels (ic_factorized_*_net, ic_conditional_*_bin).
+cfg.MODEL.ENTROPY_MODEL.DIMS and any BIN run the generic kernels
+(ic_factorized_*_net, ic_conditional_*_bin): up to 5 hidden layers of width <= 8
+with the activations in registers, larger nets (up to 31 hidden layers of width
+<= 256) with them in a workspace.
 """
 import math
 

@@ -353,25 +353,38 @@ int ic_factorized_bwd(const float* q, long long n, int C, const ic_fact_params* 
  *      layer l maps dims[l] -> dims[l+1] channels-wise, dims = {1, DIMS..., 1}; per layer
  *      w[l] [C][dims[l+1]][dims[l]], b[l] [C][dims[l+1]], f[l] [C][dims[l+1]] (NULL on the last
  *      layer: no gate).  Noise u - bin/2, mass between q -+ bin/2.  Modes as ic_factorized_fwd. */
-#define IC_FACT_MAXL 6   /* layers, len(DIMS) + 1 */
-#define IC_FACT_MAXW 8   /* hidden width */
+#define IC_FACT_MAXL 6   /* layers (len(DIMS) + 1) the register kernels take */
+#define IC_FACT_MAXW 8   /* hidden width the register kernels take */
+#define IC_FACT_NET_MAXL 32   /* layers of ic_fact_net: the wide kernels' limit */
+#define IC_FACT_WIDE_MAXW 256 /* hidden width of the wide kernels */
 typedef struct ic_fact_net {
   int nlayers;
-  int dims[IC_FACT_MAXL + 1];
-  const float* w[IC_FACT_MAXL];
-  const float* b[IC_FACT_MAXL];
-  const float* f[IC_FACT_MAXL];
+  int dims[IC_FACT_NET_MAXL + 1];
+  const float* w[IC_FACT_NET_MAXL];
+  const float* b[IC_FACT_NET_MAXL];
+  const float* f[IC_FACT_NET_MAXL];
 } ic_fact_net;
 typedef struct ic_fact_net_grads {
-  float* w[IC_FACT_MAXL];
-  float* b[IC_FACT_MAXL];
-  float* f[IC_FACT_MAXL];
+  float* w[IC_FACT_NET_MAXL];
+  float* b[IC_FACT_NET_MAXL];
+  float* f[IC_FACT_NET_MAXL];
 } ic_fact_net_grads;
+/* Geometries within IC_FACT_MAXL layers of width <= IC_FACT_MAXW run the register kernels and need no
+ * workspace; larger ones (up to IC_FACT_NET_MAXL layers of width <= IC_FACT_WIDE_MAXW) run the wide
+ * kernels, whose workspace ic_factorized_net_ws gives (bwd: 0 forward, 1 backward).  The plain entry
+ * points are the _ex ones without a workspace (IC_ERR_WORKSPACE on a wide geometry). */
+size_t ic_factorized_net_ws(long long n, int C, const ic_fact_net* net, int bwd);
 int ic_factorized_fwd_net(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
                           const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
                           void* stream);
 int ic_factorized_bwd_net(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
                           const float* dp, float* dz, const ic_fact_net_grads* grd, void* stream);
+int ic_factorized_fwd_net_ex(const float* z, long long n, int C, const ic_fact_net* net, float bin, int mode,
+                             const float* u, unsigned long long seed, unsigned long long offset, float* q, float* p,
+                             void* ws, size_t ws_bytes, void* stream);
+int ic_factorized_bwd_net_ex(const float* q, long long n, int C, const ic_fact_net* net, float bin, const float* dq,
+                             const float* dp, float* dz, const ic_fact_net_grads* grd, void* ws, size_t ws_bytes,
+                             void* stream);
 
 /* ---- quantization of the conditional model alone (entropy_model.py:331-336): q = y + (u - bin/2)
  *      (modes 0 / 2 / 3 as ic_conditional_fwd, the same draws element for element) or round(y) (mode 1) */

@@ -1,6 +1,7 @@
 """CPU-side checks of the drop-in boundary: the C-ABI library loads, exports
 every symbol include/imgcomp.h declares, and the Python mirror of the
 reference API builds with the reference's parameter names/shapes/init."""
+import ctypes
 import os
 import re
 
@@ -377,3 +378,30 @@ def test_training_step_path_has_no_ctypes_call():
     for mod in (functional, noise):
         src = inspect.getsource(mod)
         assert "ctypes" not in src and "_lib.load()" not in src and "_L()" not in src, mod.__name__
+
+
+def test_factorized_net_workspace_selects_the_kernels():
+    """ic_factorized_net_ws (host code): 0 -- the register kernels -- up to 5 hidden layers of width <= 8,
+    the wide kernels' workspace beyond, 0 past their limits (the call then returns IC_ERR_ARG)."""
+    from image_compression_amd import _lib
+    lib = _lib.load()
+
+    def ws(dims, bwd):
+        net = _lib.ICFactNet()
+        net.nlayers = len(dims) - 1
+        for i, d in enumerate(dims):
+            net.dims[i] = d
+        for l in range(net.nlayers):
+            net.w[l] = net.b[l] = net.f[l] = 256   # never dereferenced by the query
+        return lib.ic_factorized_net_ws(192 * 16, 192, ctypes.byref(net), bwd)
+
+    for bwd in (0, 1):
+        assert ws([1, 3, 3, 3, 1], bwd) == 0
+        assert ws([1, 8, 8, 8, 8, 8, 1], bwd) == 0
+        assert ws([1, 16, 16, 1], bwd) > 0
+        assert ws([1] + [3] * 7 + [1], bwd) > 0
+        assert ws([1] + [256] * 31 + [1], bwd) > 0
+        assert ws([1, 257, 1], bwd) == 0                 # past IC_FACT_WIDE_MAXW
+        net = _lib.ICFactNet()
+        net.nlayers = _lib.FACT_NET_MAXL + 1                # past IC_FACT_NET_MAXL layers
+        assert lib.ic_factorized_net_ws(192 * 16, 192, ctypes.byref(net), bwd) == 0

@@ -142,7 +142,10 @@ def test_gdn_known_answers_gpu():
 
 # (DIMS, BIN): the default runs the fused fixed-width kernels, the others the generic
 # ones (ic_factorized_*_net; entropy_model.py:88-99, :198, :229-232, :259-269)
-ENTROPY_GEOMS = [([3, 3, 3], 1.0), ([3, 3, 3], 2.0), ([2, 4, 2], 1.0), ([5], 0.5), ([8, 8, 8, 8, 8], 1.0)]
+# (8 x 5 is the register kernels' largest net; the last three run the wide kernels: a hidden width
+# past 8, more than five hidden layers, both)
+ENTROPY_GEOMS = [([3, 3, 3], 1.0), ([3, 3, 3], 2.0), ([2, 4, 2], 1.0), ([5], 0.5), ([8, 8, 8, 8, 8], 1.0),
+                 ([16, 16], 1.0), ([3] * 7, 0.5), ([40, 12, 3, 9, 5, 4], 1.0)]
 
 
 @pytest.mark.parametrize("dims,bin_", ENTROPY_GEOMS)
