@@ -44,6 +44,13 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __attribute__((aligned(16))) float edge_zero_page[4];
 __device__ __attribute__((aligned(16))) float edge_store_dump[128];  // written, never read
+#ifndef EC_STAMP
+#define EC_STAMP 0  // diagnostic build: s_memtime at six points of each unit of edge_conv_x3_kernel, per wave
+#endif
+#if EC_STAMP
+constexpr int EC_ST_IT = 40, EC_ST_N = 8;
+__device__ unsigned long long edge_stamps[256 * 8 * EC_ST_IT * EC_ST_N];
+#endif
 
 struct EdgeGeom {
   const float* x;            // few-channel image, NCHW strides (sw == 1)
@@ -385,28 +392,42 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) ob[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
   int it = 0;
+#if EC_STAMP
+  unsigned long long* const stp = edge_stamps + ((size_t)(blockIdx.x & 255) * 8 + w) * EC_ST_IT * EC_ST_N;
+#define EC_ST(k) \
+  if (lane == 0 && it < EC_ST_IT) stp[it * EC_ST_N + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define EC_ST(k)
+#endif
   for (long long u = u0; u < g.units; u += gs, ++it) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) asm volatile("" ::"v"(ob[t][j]));  // keeps `ob` apart from `acc`
+    EC_ST(0)
     // planes(u) and patch(u + gs) are in LDS; every read of plane buffer (it + 1) & 1 and patch
     // buffer it & 1 (the previous iteration's) is done
     __syncthreads();
+    EC_ST(1)
     // patch(u + 2 gs) into the buffer patch(u) occupied (its planes were built last iteration)
     edge_patch_dma(g, pm, min(u + 2 * gs, ulast), lds0 + 4u * (uint32_t)((it & 1) * bufsz), wu);
+    EC_ST(2)
     build(lds + ((it + 1) & 1) * bufsz, bpl + ((it + 1) & 1) * NP * EC3_PL);
+    EC_ST(3)
     const __bf16* planes = bpl + (it & 1) * NP * EC3_PL;
-    floatx4v acc[2][NTW];
+    const int seg = (int)(u % g.units_per_row);
+    const long long rr = u / g.units_per_row;
+    float* yb = y + (rr / g.Ho) * ys_n + (rr % g.Ho) * ys_h + nbase + 4 * lq;
+    // m-tile t outermost: t = 0's output stores issue while t = 1's MFMAs run (EC_T_OUTER; 0: all
+    // MFMAs, then one burst of 2 NTW stores)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+      floatx4v acc[NTW];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[t][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NTW; ++j) acc[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int sx = 0; sx < EC3_S; ++sx) {
-      if (sx < S) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
+      for (int sx = 0; sx < EC3_S; ++sx) {
+        if (sx < S) {
           const int p = 16 * (mt0 + t) + li;
           const int off = p * EC3_KP + 8 * ((4 * sx + lq) ^ (((p >> 3) & 1) << 1));
           eb8 bf[NP];
@@ -415,7 +436,7 @@ __global__ void __launch_bounds__(512, 1)
           if constexpr (NP == 1) {
 #pragma unroll
             for (int j = 0; j < NTW; ++j)
-              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][sx][j], bf[0], acc[t][j], 0, 0, 0);
+              acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][sx][j], bf[0], acc[j], 0, 0, 0);
           } else {
             // the six products, smallest first (a dependent MFMA issues back to back)
             constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
@@ -423,30 +444,23 @@ __global__ void __launch_bounds__(512, 1)
             for (int j = 0; j < NTW; ++j)
 #pragma unroll
               for (int pr6 = 0; pr6 < 6; ++pr6)
-                acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[PA[pr6]][sx][j], bf[PB[pr6]], acc[t][j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[PA[pr6]][sx][j], bf[PB[pr6]], acc[j], 0, 0, 0);
           }
         }
       }
-    }
-    // epilogue: C/D map row n = 4lq + r (channel), col = li (pixel 16mt + li).  The stored values
-    // stay in registers of their own (`ob`, live across the unit loop): overwriting a store's data
-    // registers waits for the store
+      // epilogue of m-tile t: C/D map row n = 4lq + r (channel), col = li (pixel 16 (mt0 + t) + li).  The
+      // stored values stay in registers of their own (`ob`, live across the unit loop): overwriting a
+      // store's data registers waits for the store
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const floatx4v bv = *(const floatx4v*)(bl + nbase + 16 * j + 4 * lq);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int j = 0; j < NTW; ++j) {
+        const floatx4v bv = *(const floatx4v*)(bl + nbase + 16 * j + 4 * lq);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = acc[t][j][r] + bv[r];
+          const float x = acc[j][r] + bv[r];
           ob[t][j][r] = (relu && !(x > 0.f)) ? 0.f : x;  // branch-free ReLU
         }
-    }
-    const int seg = (int)(u % g.units_per_row);
-    const long long rr = u / g.units_per_row;
-    float* yb = y + (rr / g.Ho) * ys_n + (rr % g.Ho) * ys_h + nbase + 4 * lq;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
+      }
+      EC_ST(4)
       const int ox = seg * SEG + 16 * (mt0 + t) + li;
       // branch-free: pixels past the row store into a dump slot (no exec-masked memory operation,
       // so the waitcnt pass counts the stores exactly)
@@ -454,14 +468,17 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) *(floatx4v*)(dst + 16 * j) = ob[t][j];
     }
+    EC_ST(5)
     // the patch DMA issued at the top of this iteration must have landed before the barrier (the next
     // iteration builds from it); the 2 NTW output stores issued after it may stay in flight.  vmcnt
     // counts loads and stores in issue order: with the round-5 register-staged patch the compiler's
     // wait for the patch loads (vmcnt(0) at the loop's merge) also waited for the previous unit's
     // 48 KB of output stores (round 6: g_a.0 fwd 0.174 -> 0.170 ms alternating, r09e; the kernel is
     // bound by its MFMA and store energy rather than by that wait: profiles/r09c_x3d_edge_ablations.txt)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NTW) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NTW + (EC_STAMP ? 4 : 0)) : "memory");
+    EC_ST(6)
   }
+#undef EC_ST
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -1235,3 +1252,11 @@ int tconv_few_run(const float* x, int N, int Hin, int Win, int Cin, const float*
   return IC_OK;
 }
 
+
+#if EC_STAMP
+// diagnostic build only (EC_STAMP): the edge conv's s_memtime stamps, for tools/edge_stamps.py
+extern "C" int ic_debug_edge_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(edge_stamps)) bytes = sizeof(edge_stamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(edge_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
