@@ -501,7 +501,7 @@ size_t need_or_zero(int rc, size_t n) { return rc ? 0 : n; }
 
 extern "C" {
 
-int ic_version(void) { return 2; }
+int ic_version(void) { return 3; }  // 3: ic_fact_net / ic_fact_net_grads hold IC_FACT_NET_MAXL layers (round 6)
 
 int ic_conv_plan(int op, const ic_act* a, const ic_act* b, int k, int stride, int pad, int math, ic_plan* out) {
   if (!out || !a || (!b && op != IC_OP_GDN_FWD && op != IC_OP_GDN_BWD)) return IC_ERR_ARG;

@@ -54,7 +54,7 @@ typedef struct ic_act {
 } ic_act;
 
 /* ---- library ---- */
-int ic_version(void);                 /* ABI version (monotonic) */
+int ic_version(void);                 /* ABI version (monotonic; 3: ic_fact_net with IC_FACT_NET_MAXL layers) */
 int ic_device_sync_check(void* stream); /* hipStreamQuery-free no-op launch test */
 
 /* ---- Conv2d (k x k, stride, zero pad): y = conv(x, w) + b, act 0=none 1=relu

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     # every declared symbol has a ctypes signature and vice versa
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert lib.ic_version() >= 1
+    assert lib.ic_version() >= 3  # the ctypes structs in _lib.py mirror the version-3 layout
 
 
 def test_workspace_queries_without_gpu():
