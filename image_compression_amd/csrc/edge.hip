@@ -320,7 +320,17 @@ __global__ void __launch_bounds__(512, 1)
   const int zero_off = PSZ;
   const int bufsz = PMAX + 2 * SEG * 2;
 
-  // split weights as A fragments: aw[part][sx][j] = plane part of wp[n = nbase + 16 j + li][32 sx + 8 lq .. + 7]
+  // split weights as A fragments: aw[part][sx][j] = plane part of wp[n = nbase + 16 j + li][32 sx + 8 lq .. + 7].
+  // All 72 loads first, unconditional (index clamped into the row), the zero fill after: a load under a
+  // per-element condition became a branch and a vmcnt(0) wait each, 72 L2 round trips in series per block
+  float wv[EC3_S][NTW][8];
+#pragma unroll
+  for (int sx = 0; sx < EC3_S; ++sx)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        wv[sx][j][e] = wp[(size_t)(nbase + 16 * j + li) * Kp + min(32 * sx + 8 * lq + e, Kp - 1)];
   eb8 aw[NP][EC3_S][NTW];
 #pragma unroll
   for (int sx = 0; sx < EC3_S; ++sx)
@@ -329,7 +339,7 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int kq = 32 * sx + 8 * lq + e;
-        const float v = (sx < S && kq < Kp) ? wp[(size_t)(nbase + 16 * j + li) * Kp + kq] : 0.f;
+        const float v = (sx < S && kq < Kp) ? wv[sx][j][e] : 0.f;
         if constexpr (NP == 1) {
           aw[0][sx][j][e] = (__bf16)v;  // round to nearest even
         } else {

@@ -509,11 +509,14 @@ __device__ __forceinline__ void ig_epilogue16(const IgDesc& d, const IgPhase& P,
   if (d.epi == EPI_NONE || d.epi == EPI_RELU) {
     float bj[TN];
     bool nok[TN];
+    // the bias loads unconditional (index clamped; columns past Cout are never stored) under one uniform
+    // test: a load per lane-dependent condition became a branch and a vmcnt(0) wait each, in series
+    const float* __restrict__ bias = d.bias;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 16 + c16;
       nok[j] = n < d.Cout;
-      bj[j] = (d.bias && nok[j]) ? d.bias[n] : 0.f;
+      bj[j] = bias ? bias[min(n, d.Cout - 1)] : 0.f;
     }
     const bool relu = d.epi == EPI_RELU;
 #pragma unroll

@@ -108,27 +108,34 @@ __global__ void __launch_bounds__(PK_NT) pack_tile_kernel(const PackArgs p) {
   const int valid = p.mode == 0 ? min(PK_TR, R - r0) * kk : max(0, min(PK_TN, Nout - n0)) * kk;
   const int col0 = p.mode == 0 ? r0 : n0;
   const int nv = nrows * (len >> 2);
-#pragma unroll 4
-  for (int j = tid; j < nv; j += PK_NT) {
-    const int row = j / (len >> 2), q = 4 * (j - row * (len >> 2));
-    const int gr = row0 + row;
-    const float* src = p.W + ((long long)gr * p.B + col0) * kk + q;
-    float v[4];
-    if (gr < rowmax && q + 3 < valid) {
-      const float4 t = *(const float4*)src;
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-    } else {
+  // every load unconditional, at an index clamped into W, the zero fill by select: loads under a
+  // per-element condition became branches with a vmcnt(0) wait each (49 in series per thread)
+  constexpr int NIT = (PK_TN * PK_TR * 25 / 4 + PK_NT - 1) / PK_NT;  // float4 groups per thread (k <= 5)
+  const long long wlast = (long long)p.A * p.B * kk - 1;
+  float v[NIT][4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (gr < rowmax && q + e < valid) ? src[e] : 0.f;
-    }
+  for (int it = 0; it < NIT; ++it) {
+    const int j = min(tid + PK_NT * it, nv - 1);
+    const int row = j / (len >> 2), q = 4 * (j - row * (len >> 2));
+    const long long base = ((long long)min(row0 + row, rowmax - 1) * p.B + col0) * kk + q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[it][e] = p.W[min(base + e, wlast)];
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int j = tid + PK_NT * it;
+    if (j >= nv) continue;
+    const int row = j / (len >> 2), q = 4 * (j - row * (len >> 2));
+    const bool rok = row0 + row < rowmax;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int qq = q + e;
+      const float x = (rok && qq < valid) ? v[it][e] : 0.f;
       if (p.mode == 0) {
-        ws[row * len + qq] = v[e];  // [nl][rl][tap]
+        ws[row * len + qq] = x;  // [nl][rl][tap]
       } else {
         const int nl = qq / kk, tap = qq - nl * kk;
-        ws[(nl * PK_TR + row) * kk + tap] = v[e];
+        ws[(nl * PK_TR + row) * kk + tap] = x;
       }
     }
   }
