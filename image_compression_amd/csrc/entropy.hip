@@ -197,25 +197,37 @@ __global__ void __launch_bounds__(256) fact_bwd_k(const float* qin, long long n,
   }
   block_sum<NG>(G, lds);
   if (threadIdx.x == 0) {
+    // every parameter read before the first gradient store (the stores may alias the parameters as far
+    // as the compiler knows, so interleaved they serialised each load behind the store before it)
+    float w0[3], w3[3], f0[3], f1[3], f2[3], w1[9], w2[9];
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      const float w0 = P.w0[c * 3 + o], w3 = P.w3[c * 3 + o];
-      GR.w0[c * 3 + o] = G[0 + o] * dsoftplusf(w0);
-      GR.b0[c * 3 + o] = G[3 + o];
-      const float t0 = tanhf(P.f0[c * 3 + o]);
-      GR.f0[c * 3 + o] = G[6 + o] * (1.f - t0 * t0);
-      GR.b1[c * 3 + o] = G[18 + o];
-      const float t1 = tanhf(P.f1[c * 3 + o]);
-      GR.f1[c * 3 + o] = G[21 + o] * (1.f - t1 * t1);
-      GR.b2[c * 3 + o] = G[33 + o];
-      const float t2 = tanhf(P.f2[c * 3 + o]);
-      GR.f2[c * 3 + o] = G[36 + o] * (1.f - t2 * t2);
-      GR.w3[c * 3 + o] = G[39 + o] * dsoftplusf(w3);
+      w0[o] = P.w0[c * 3 + o]; w3[o] = P.w3[c * 3 + o];
+      f0[o] = P.f0[c * 3 + o]; f1[o] = P.f1[c * 3 + o]; f2[o] = P.f2[c * 3 + o];
     }
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-      GR.w1[c * 9 + j] = G[9 + j] * dsoftplusf(P.w1[c * 9 + j]);
-      GR.w2[c * 9 + j] = G[24 + j] * dsoftplusf(P.w2[c * 9 + j]);
+      w1[j] = P.w1[c * 9 + j];
+      w2[j] = P.w2[c * 9 + j];
+    }
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      GR.w0[c * 3 + o] = G[0 + o] * dsoftplusf(w0[o]);
+      GR.b0[c * 3 + o] = G[3 + o];
+      const float t0 = tanhf(f0[o]);
+      GR.f0[c * 3 + o] = G[6 + o] * (1.f - t0 * t0);
+      GR.b1[c * 3 + o] = G[18 + o];
+      const float t1 = tanhf(f1[o]);
+      GR.f1[c * 3 + o] = G[21 + o] * (1.f - t1 * t1);
+      GR.b2[c * 3 + o] = G[33 + o];
+      const float t2 = tanhf(f2[o]);
+      GR.f2[c * 3 + o] = G[36 + o] * (1.f - t2 * t2);
+      GR.w3[c * 3 + o] = G[39 + o] * dsoftplusf(w3[o]);
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      GR.w1[c * 9 + j] = G[9 + j] * dsoftplusf(w1[j]);
+      GR.w2[c * 9 + j] = G[24 + j] * dsoftplusf(w2[j]);
     }
     GR.b3[c] = G[42];
   }
