@@ -352,7 +352,10 @@ constexpr int FMAX = 11;                      // fused kernels: filter size 11 (
 constexpr int FTW = 64, FTH = 16;             // forward: valid outputs per tile
 constexpr int FRW = FTW + FMAX - 1, FRH = FTH + FMAX - 1;
 constexpr int FAP = 76;                       // forward input pitch (>= FRW, four-aligned 14-wide windows)
-constexpr int BTW = 32, BTH = 16;             // backward: gradient pixels per tile
+// backward: gradient pixels per tile.  32 x 22: the phases' work items (42 x 11 moment rows, 32 x 11
+// derivative rows, 22 x 11 adjoint rows, 22 x 8 output groups) take as many 256-thread rounds as 32 x 16
+// took (2, 2, 1, 1) for 1.375x the pixels; 78 KB of LDS, two blocks per CU
+constexpr int BTW = 32, BTH = 22;
 constexpr int BDW = BTW + FMAX - 1, BDH = BTH + FMAX - 1;          // derivative-map region
 constexpr int BDP = 44;                       // its pitch: 11 groups of four columns
 constexpr int BIW = BTW + 2 * (FMAX - 1), BIH = BTH + 2 * (FMAX - 1);  // input region
