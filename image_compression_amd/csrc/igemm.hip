@@ -1109,6 +1109,71 @@ __global__ void ig_reduce_kernel(const IgDesc d) {
   }
 }
 
+#ifndef IG_REDUCE4
+#define IG_REDUCE4 1
+#endif
+// the same reduction on float4 columns (Cout % 4 == 0): four channels per thread, the splits summed per
+// channel in ig_reduce_kernel's order (split s into accumulator s & 7, then the fixed tree), so the result
+// is bitwise the same; KS > 0: the split count at compile time (every load issued before the first add)
+template <int KS>
+__global__ void __launch_bounds__(256) ig_reduce4_kernel(const IgDesc d) {
+  const int ks = KS ? KS : d.ksplit;
+  const int c4n = d.Cout >> 2;
+  const long long total4 = d.Mtot * c4n;
+  const floatx4v* __restrict__ part = (const floatx4v*)d.partial;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total4;
+       i += (long long)gridDim.x * blockDim.x) {
+    floatx4v a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (KS > 0) {
+      floatx4v v[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) v[s] = part[i + s * total4];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s & 7] += v[s];
+    } else {
+      int s = 0;
+      for (; s + 7 < ks; s += 8) {
+        floatx4v v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[i + (s + j) * total4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += v[j];
+      }
+      // the rest (< 8, a uniform count): clamped loads, each added only where it exists
+      floatx4v v[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) v[j] = part[i + min(s + j, ks - 1) * total4];
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        if (s + j < ks) a[j] += v[j];
+    }
+    const floatx4v v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    const long long mg = i / c4n;
+    const int n = (int)(i - mg * c4n) * 4;
+    int ph = 0;
+#pragma unroll
+    for (int q = 1; q < IC_MAXPH; ++q)
+      if (q < d.nphase && mg >= d.ph[q].m_off) ph = q;
+    const IgPhase& P = d.ph[ph];
+    const uint32_t m = (uint32_t)(mg - P.m_off);
+    const uint32_t ob = ig_out_offset(d, P, m) + (uint32_t)n * (uint32_t)d.ys_c;
+    if ((d.epi == EPI_NONE || d.epi == EPI_RELU) && d.ys_c == 1 && ((uintptr_t)(d.y + ob) & 15) == 0 &&
+        ((uintptr_t)d.bias & 15) == 0) {
+      floatx4v o = v;
+      if (d.bias) o += *(const floatx4v*)(d.bias + n);
+      if (d.epi == EPI_RELU)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
+      *(floatx4v*)(d.y + ob) = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ig_store_out(d, v[e], ob + (uint32_t)e * (uint32_t)d.ys_c, n + e);
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 int ig_launch_t(const IgDesc& d, hipStream_t s) {
   int mt = 0;
@@ -1279,6 +1344,20 @@ int ig_run(IgDesc& d, hipStream_t s) {
   if (rc) return rc;
   if (d.ksplit > 1) {
     const long long total = d.Mtot * d.Cout;
+    if (IG_REDUCE4 && d.Cout % 4 == 0 && ((uintptr_t)d.partial & 15) == 0) {
+      long long blocks = (total / 4 + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      const dim3 g((unsigned)blocks), b(256);
+      switch (d.ksplit) {
+        case 2: hipLaunchKernelGGL(ig_reduce4_kernel<2>, g, b, 0, s, d); break;
+        case 3: hipLaunchKernelGGL(ig_reduce4_kernel<3>, g, b, 0, s, d); break;
+        case 4: hipLaunchKernelGGL(ig_reduce4_kernel<4>, g, b, 0, s, d); break;
+        case 8: hipLaunchKernelGGL(ig_reduce4_kernel<8>, g, b, 0, s, d); break;
+        default: hipLaunchKernelGGL(ig_reduce4_kernel<0>, g, b, 0, s, d);
+      }
+      IC_CHECK_LAUNCH();
+      return IC_OK;
+    }
     long long blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(ig_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d);
